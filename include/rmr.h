@@ -1,0 +1,157 @@
+/*
+ * rmr.h — C ABI of the MI355X-native SDF ray-march path tracer (librmr.so).
+ *
+ * This is the drop-in boundary for the reference's render backend, the static C++ class
+ * `Graphics` (RayMarch Renderer/Graphics.h:15-134, Graphics.cpp:215-835), which had no FFI of its
+ * own. Each entry point names the reference member it replaces. Conventions:
+ *   - plain C, opaque handle, int status (RMR_OK = 0, negative = error), message through
+ *     rmr_last_error(ctx); nothing throws across the boundary;
+ *   - caller-owned host buffers, library-owned device memory (or caller-bound device memory via
+ *     rmr_bind_accum), one context per thread;
+ *   - calls are asynchronous w.r.t. the GPU exactly like the reference's glDispatchCompute;
+ *     rmr_sync / rmr_read_accum / rmr_save_bmp synchronise.
+ * INTEGRATION.md shows the binding a maintainer adds on the reference side.
+ */
+#ifndef RMR_H
+#define RMR_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "rmr_tables.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMR_OK          0
+#define RMR_E_INVALID  (-1) /* bad argument                                                  */
+#define RMR_E_HIP      (-2) /* HIP runtime error / no device                                  */
+#define RMR_E_SCENE    (-3) /* scene does not compile (the reference's shader compile error)  */
+#define RMR_E_IO       (-4) /* file I/O                                                        */
+#define RMR_E_STATE    (-5) /* call out of order (e.g. render before a scene is loaded)        */
+#define RMR_E_NOMEM    (-6)
+#define RMR_E_UNSUPPORTED (-7)
+
+typedef struct rmr_ctx rmr_ctx;
+
+/* Render parameters. Defaults = the constants Graphics::Render uploads (Graphics.cpp:326-340). */
+typedef struct rmr_params {
+    float   max_dist;          /* 1000                                                        */
+    int32_t max_steps;         /* 512                                                         */
+    int32_t max_bounces;       /* 16                                                          */
+    float   step_multiply;     /* 0.5                                                         */
+    int32_t separate_channels; /* 0                                                           */
+    int32_t use_env_tex;       /* 0 (env-map sky is not supported yet: RMR_E_UNSUPPORTED)     */
+} rmr_params;
+
+/* Kernel statistics for the roofline (accumulated since the last rmr_reset_stats). */
+typedef struct rmr_stats {
+    uint64_t map_evals;      /* scene-SDF evaluations (the algorithmic work unit)  */
+    uint64_t samples;        /* pixel samples traced                                           */
+    uint64_t trace_launches; /* trace-kernel launches                                          */
+    double   trace_ms;       /* summed trace-kernel time measured with HIP events              */
+    double   fold_ms;        /* summed accumulate-kernel time                                  */
+    double   flops_per_map;  /* algorithmic flops of one map() for the loaded scene            */
+} rmr_stats;
+
+/* ---- lifetime --------------------------------------------------------------------------- */
+/* Graphics::Init (Graphics.cpp:263-300): select device, create streams; no GL context needed. */
+int  rmr_create(rmr_ctx** out, int device);
+void rmr_destroy(rmr_ctx* ctx);
+const char* rmr_last_error(const rmr_ctx* ctx);
+/* Compile-time kernel configuration string (variants, wave size, build flags). */
+const char* rmr_build_info(void);
+
+/* Run kernels on a caller stream (a hipStream_t passed as void*; NULL = library stream). */
+int rmr_set_stream(rmr_ctx* ctx, void* hip_stream);
+
+/* ---- image / view / params ------------------------------------------------------------- */
+/* Graphics::setImageSize / getImageSize (Graphics.cpp:817-825). The reference applies a new size
+ * at the next Init/Reload (Graphics.cpp:744-745); rmr_reload does the same here. */
+int rmr_set_image_size(rmr_ctx* ctx, int w, int h);
+int rmr_get_image_size(const rmr_ctx* ctx, int* w, int* h);
+
+int rmr_set_params(rmr_ctx* ctx, const rmr_params* p);
+int rmr_get_params(const rmr_ctx* ctx, rmr_params* p);
+void rmr_default_params(rmr_params* p);
+
+/* Graphics::setView (Graphics.cpp:827-835), arguments in *shader-uniform* order. Note the
+ * reference camera calls setView(eye, ray00, ray10, ray01, ray11) (Camera.cpp:101), so its
+ * uniform "ray01" holds the camera's ray10. rmr_camera_view() below already applies that swap. */
+int rmr_set_view(rmr_ctx* ctx, const float eye[3], const float ray00[3], const float ray01[3],
+                 const float ray10[3], const float ray11[3]);
+
+/* Camera::calculateRays (Camera.cpp:25-102) restated: eye/dir/aspect/fov -> the five uniforms in
+ * shader order (eye, ray00, ray01, ray10, ray11), i.e. after the setView argument swap. */
+void rmr_camera_view(const double eye[3], const double dir[3], float aspect, float fov,
+                     float out_eye[3], float out_ray00[3], float out_ray01[3],
+                     float out_ray10[3], float out_ray11[3]);
+
+/* ---- scene ------------------------------------------------------------------------------- */
+/* Graphics::clearScene/addMaterial/addObject + Reload's code generator (Graphics.cpp:392-752,
+ * 801-815): parse a reference scene file (v1 or v2 format, App. C of SURVEY) for `variant` and
+ * compile it into tables. Errors the reference would hit as a GLSL compile error (stale arity,
+ * unknown node, bad var index) return RMR_E_SCENE with the message in rmr_last_error. */
+int rmr_load_scene_json(rmr_ctx* ctx, int variant, const char* json, size_t len);
+/* Load precompiled tables (copied). */
+int rmr_load_scene_tables(rmr_ctx* ctx, const rmr_scene* scene);
+/* The built-in scenes that the reference hard-codes in its shaders: RM2's one-sphere map
+ * (RayMarch2.glsl:133-172, needs a v2 material for id 1 via rmr_load_scene_json) and RM3's
+ * three-primitive spectral scene (RayMarch3.glsl:132-143, 251-345). */
+int rmr_load_builtin_scene(rmr_ctx* ctx, int variant);
+
+/* Graphics::Reload tail (Graphics.cpp:741-751): apply the pending image size and clear the
+ * accumulator to (0,0,0,0). */
+int rmr_reload(rmr_ctx* ctx);
+
+/* ---- render ------------------------------------------------------------------------------ */
+/* Graphics::Render (Graphics.cpp:314-354): add ONE sample to every pixel with
+ * min <= pix < max, as the running mean of RayMarch*.glsl main() using `current_sample` (0
+ * overwrites). `time` is the rand() seed uniform. */
+int rmr_render(rmr_ctx* ctx, float time, float min_x, float min_y, float max_x, float max_y,
+               uint32_t current_sample);
+/* Batched fast path: samples first_sample .. first_sample+nspp-1 of every pixel in the integer
+ * rect [x0,x1)x[y0,y1), sample k seeded with times[k]. Bitwise equal to nspp rmr_render calls
+ * with the same times. */
+int rmr_render_spp(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1,
+                   uint32_t first_sample, uint32_t nspp);
+/* Same as rmr_render_spp but over an explicit tile list (tile_size x tile_size tiles, given as
+ * (tx,ty) pairs): the multi-GPU partition unit. */
+int rmr_render_tiles(rmr_ctx* ctx, const float* times, const int32_t* tiles_xy, int n_tiles,
+                     int tile_size, uint32_t first_sample, uint32_t nspp);
+
+/* ---- output ------------------------------------------------------------------------------ */
+/* Accumulator as RGBA32F, row 0 = image row 0 (= the top edge). */
+int rmr_read_accum(rmr_ctx* ctx, float* rgba, size_t bytes);
+int rmr_write_accum(rmr_ctx* ctx, const float* rgba, size_t bytes); /* checkpoint resume */
+/* Device pointer of the accumulator (float4 per pixel) for collectives (RCCL reduce). */
+void* rmr_accum_device_ptr(rmr_ctx* ctx);
+/* Render into caller-owned device memory of w*h*16 bytes instead (e.g. a torch tensor). */
+int rmr_bind_accum(rmr_ctx* ctx, void* device_ptr, size_t bytes);
+/* Graphics::SaveImage (Graphics.cpp:754-799): 24-bit BMP with the reference's quirks
+ * (u8 round, 1.055*c^(1/2.4) without -0.055, truncation, SOIL pink background for alpha 0). */
+int rmr_save_bmp(rmr_ctx* ctx, const char* path);
+/* The same encoding from a host RGBA32F buffer (no context needed). */
+int rmr_encode_bmp(const float* rgba, int w, int h, const char* path);
+/* Raw float accumulator checkpoint: "RMRACC1\0", w, h, samples, then RGBA32F. */
+int rmr_save_accum(rmr_ctx* ctx, const char* path, uint32_t samples_done);
+int rmr_load_accum(rmr_ctx* ctx, const char* path, uint32_t* samples_done);
+
+int rmr_sync(rmr_ctx* ctx);
+int rmr_get_stats(rmr_ctx* ctx, rmr_stats* out);
+int rmr_reset_stats(rmr_ctx* ctx);
+/* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */
+int rmr_set_kernel(rmr_ctx* ctx, int kernel);
+/* Tuning knobs (<= 0 / < 0 keeps the current value): deferred-shading batch size in lanes (1..64),
+ * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. */
+int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long samp_budget_bytes);
+/* Test hook: per-sample radiance (before the running mean) of the integer rect, written as
+ * out[k][y-y0][x-x0][4]; sample k is seeded with times[k]. The accumulator is left unchanged. */
+int rmr_trace_samples(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out);
+/* sizeof of the ABI structs (prim, op, material, spectral, rm2_consts, scene, params, stats). */
+int rmr_abi_sizes(int32_t* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMR_H */

@@ -1,0 +1,89 @@
+"""ctypes binding of librmr.so (the C ABI in include/rmr.h).
+
+librmr.so is built in-tree by raymarchrenderer_amd/csrc/Makefile (``__graft_entry__.build()``).
+There is no fallback: if the library is missing, every entry point raises.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librmr.so")
+_lib = None
+
+EXPORTS = [
+    "rmr_create", "rmr_destroy", "rmr_last_error", "rmr_build_info", "rmr_set_stream",
+    "rmr_set_image_size", "rmr_get_image_size", "rmr_set_params", "rmr_get_params",
+    "rmr_default_params", "rmr_set_view", "rmr_camera_view", "rmr_load_scene_json",
+    "rmr_load_scene_tables", "rmr_load_builtin_scene", "rmr_reload", "rmr_render",
+    "rmr_render_spp", "rmr_render_tiles", "rmr_read_accum", "rmr_write_accum",
+    "rmr_accum_device_ptr", "rmr_bind_accum", "rmr_save_bmp", "rmr_encode_bmp",
+    "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats",
+    "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes",
+]
+
+
+class RMRError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (abi.ERRORS.get(code, "RMR_E?"), code, msg))
+        self.code = code
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "csrc"), "-j8"])
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("librmr.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(expected at %s)" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, fp, ip = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)
+    dp = C.POINTER(C.c_double)
+    sig = {
+        "rmr_create": (C.c_int, [C.POINTER(vp), C.c_int]),
+        "rmr_destroy": (None, [vp]),
+        "rmr_last_error": (C.c_char_p, [vp]),
+        "rmr_build_info": (C.c_char_p, []),
+        "rmr_set_stream": (C.c_int, [vp, vp]),
+        "rmr_set_image_size": (C.c_int, [vp, C.c_int, C.c_int]),
+        "rmr_get_image_size": (C.c_int, [vp, ip, ip]),
+        "rmr_set_params": (C.c_int, [vp, C.POINTER(abi.Params)]),
+        "rmr_get_params": (C.c_int, [vp, C.POINTER(abi.Params)]),
+        "rmr_default_params": (None, [C.POINTER(abi.Params)]),
+        "rmr_set_view": (C.c_int, [vp, fp, fp, fp, fp, fp]),
+        "rmr_camera_view": (None, [dp, dp, C.c_float, C.c_float, fp, fp, fp, fp, fp]),
+        "rmr_load_scene_json": (C.c_int, [vp, C.c_int, C.c_char_p, C.c_size_t]),
+        "rmr_load_scene_tables": (C.c_int, [vp, C.POINTER(abi.Scene)]),
+        "rmr_load_builtin_scene": (C.c_int, [vp, C.c_int]),
+        "rmr_reload": (C.c_int, [vp]),
+        "rmr_render": (C.c_int, [vp, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_uint32]),
+        "rmr_render_spp": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32]),
+        "rmr_render_tiles": (C.c_int, [vp, fp, C.POINTER(C.c_int32), C.c_int, C.c_int, C.c_uint32, C.c_uint32]),
+        "rmr_read_accum": (C.c_int, [vp, fp, C.c_size_t]),
+        "rmr_write_accum": (C.c_int, [vp, fp, C.c_size_t]),
+        "rmr_accum_device_ptr": (vp, [vp]),
+        "rmr_bind_accum": (C.c_int, [vp, vp, C.c_size_t]),
+        "rmr_save_bmp": (C.c_int, [vp, C.c_char_p]),
+        "rmr_encode_bmp": (C.c_int, [fp, C.c_int, C.c_int, C.c_char_p]),
+        "rmr_save_accum": (C.c_int, [vp, C.c_char_p, C.c_uint32]),
+        "rmr_load_accum": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_uint32)]),
+        "rmr_sync": (C.c_int, [vp]),
+        "rmr_get_stats": (C.c_int, [vp, C.POINTER(abi.Stats)]),
+        "rmr_reset_stats": (C.c_int, [vp]),
+        "rmr_set_kernel": (C.c_int, [vp, C.c_int]),
+        "rmr_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_longlong]),
+        "rmr_trace_samples": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, fp]),
+        "rmr_abi_sizes": (C.c_int, [C.POINTER(C.c_int32), C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L

@@ -1,0 +1,669 @@
+// rmr_api.cpp — the C ABI of librmr.so (include/rmr.h): the drop-in replacement for the
+// reference's static `Graphics` backend (Graphics.h:15-134, Graphics.cpp:215-835).
+//
+// Ownership: the context owns its HIP stream, the scene tables in HBM, the per-sample radiance
+// planes and (unless rmr_bind_accum is used) the RGBA32F accumulator. Host buffers passed in are
+// caller-owned and copied. No exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <new>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/rmr.h"
+#include "rmr_internal.h"
+#include "scene.hpp"
+
+namespace rmr {
+hipError_t launch_trace(const KParams& P, int variant, bool persistent, int grid, hipStream_t s);
+hipError_t launch_fold(const KParams& P, hipStream_t s);
+int trace_occupancy(int variant, int* blocks_per_cu);
+}  // namespace rmr
+
+using rmr::CompiledScene;
+using rmr::KParams;
+using rmr::TileXY;
+
+struct EventPair { hipEvent_t a, b, c; };
+
+struct rmr_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int W = 1024, H = 1024;               // GUI.cpp:201-208 defaults (Graphics.cpp:6 is overridden)
+    int pend_W = 1024, pend_H = 1024;
+    rmr_params params{};
+    float view[15];
+    bool view_set = false;
+    CompiledScene scene;
+    bool scene_loaded = false;
+    // device tables
+    rmr_prim* d_prims = nullptr;
+    rmr_op* d_ops = nullptr;
+    float* d_consts = nullptr;
+    rmr_material* d_mats = nullptr;
+    rmr_spectral* d_spec = nullptr;
+    rmr_rm2_consts* d_rm2 = nullptr;
+    // buffers
+    float4* d_accum = nullptr;
+    bool accum_external = false;
+    float4* d_samp = nullptr;
+    size_t samp_cap = 0;
+    TileXY* d_tiles = nullptr;
+    size_t tiles_cap = 0;
+    std::vector<TileXY> tiles_host;
+    float* d_times = nullptr;
+    size_t times_cap = 0;
+    unsigned long long* d_queue = nullptr;
+    unsigned long long* d_counters = nullptr;
+    // timing
+    std::vector<EventPair> pending, pool;
+    rmr_stats stats{};
+    int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
+    int shade_threshold = 24;
+    int grid_per_cu = 0;  // 0 = occupancy
+    size_t samp_budget = (size_t)8 << 30;
+    std::string err;
+};
+
+namespace {
+
+int fail(rmr_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    return code;
+}
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return fail(ctx, RMR_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dev_upload(rmr_ctx* c, T** dst, const T* src, size_t n) {
+    if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
+    const size_t bytes = std::max<size_t>(1, n) * sizeof(T);
+    HIPCHK(c, hipMalloc((void**)dst, bytes));
+    if (n) HIPCHK(c, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return RMR_OK;
+}
+
+int alloc_accum(rmr_ctx* c) {
+    if (!c->accum_external && c->d_accum) { (void)hipFree(c->d_accum); c->d_accum = nullptr; }
+    c->accum_external = false;
+    const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+    HIPCHK(c, hipMalloc((void**)&c->d_accum, bytes));
+    HIPCHK(c, hipMemsetAsync(c->d_accum, 0, bytes, c->stream));
+    return RMR_OK;
+}
+
+void default_view(rmr_ctx* c) {
+    // Program.cpp:102: Camera((0,4,-6), normalized(0,-3,6), W/H, PI/4), PI = 3.141592653f
+    const double m = std::sqrt(0.0 + 9.0 + 36.0);
+    const double eye[3] = {0.0, 4.0, -6.0};
+    const double dir[3] = {0.0, -3.0 / m, 6.0 / m};
+    const float pi = 3.141592653f;
+    rmr_camera_view(eye, dir, (float)((double)c->W / (double)c->H), pi / 4.0f, c->view, c->view + 3, c->view + 6,
+                    c->view + 9, c->view + 12);
+    c->view_set = true;
+}
+
+int upload_scene(rmr_ctx* c) {
+    const CompiledScene& s = c->scene;
+    int r;
+    if ((r = dev_upload(c, &c->d_prims, s.prims.data(), s.prims.size()))) return r;
+    if ((r = dev_upload(c, &c->d_ops, s.ops.data(), s.ops.size()))) return r;
+    if ((r = dev_upload(c, &c->d_consts, s.consts.data(), s.consts.size()))) return r;
+    if ((r = dev_upload(c, &c->d_mats, s.materials.data(), s.materials.size()))) return r;
+    if ((r = dev_upload(c, &c->d_spec, s.spectral.data(), s.spectral.size()))) return r;
+    if ((r = dev_upload(c, &c->d_rm2, &s.rm2, 1))) return r;
+    c->scene_loaded = true;
+    c->stats.flops_per_map = s.flops_per_map();
+    return RMR_OK;
+}
+
+int validate_scene(rmr_ctx* c, const CompiledScene& s) {
+    for (const auto& p : s.prims) {
+        if (p.type < RMR_PRIM_SPHERE || p.type > RMR_PRIM_MANDELBULB) return fail(c, RMR_E_SCENE, "bad prim type");
+        if (p.type == RMR_PRIM_PROGRAM) {
+            if (p.prog_begin < 0 || p.prog_end > (int)s.ops.size() || p.prog_begin > p.prog_end)
+                return fail(c, RMR_E_SCENE, "prim program range out of bounds");
+            if (p.dist_var < 0 || p.dist_var >= RMR_MAX_VARS) return fail(c, RMR_E_SCENE, "bad dist_var");
+        }
+    }
+    const int nconst = (int)(s.consts.size() / 3);
+    for (const auto& o : s.ops) {
+        for (int i = 0; i < 7; i++) {
+            const int r = o.in[i];
+            if (r == RMR_OPND_NONE || r == RMR_OPND_P) continue;
+            if (RMR_OPND_IS_CONST(r)) {
+                if (RMR_OPND_CONST_INDEX(r) >= nconst) return fail(c, RMR_E_SCENE, "constant index out of range");
+            } else if (r < 0 || r >= RMR_MAX_VARS) {
+                return fail(c, RMR_E_SCENE, "var index out of range");
+            }
+        }
+        for (int i = 0; i < 4; i++)
+            if (o.out[i] >= RMR_MAX_VARS) return fail(c, RMR_E_SCENE, "var index out of range");
+    }
+    for (const auto& m : s.materials)
+        if (m.defined && (m.prog_begin < 0 || m.prog_end > (int)s.ops.size())) return fail(c, RMR_E_SCENE, "material program range");
+    if (s.variant == RMR_VARIANT_RM2 && (s.v2_begin < 0 || s.v2_end > (int)s.ops.size()))
+        return fail(c, RMR_E_SCENE, "v2 program range");
+    return RMR_OK;
+}
+
+int ensure_samp(rmr_ctx* c, size_t n) {
+    if (n <= c->samp_cap) return RMR_OK;
+    if (c->d_samp) { (void)hipFree(c->d_samp); c->d_samp = nullptr; c->samp_cap = 0; }
+    HIPCHK(c, hipMalloc((void**)&c->d_samp, n * sizeof(float4)));
+    c->samp_cap = n;
+    return RMR_OK;
+}
+
+int set_tiles(rmr_ctx* c, const std::vector<TileXY>& t) {
+    if (t.size() == c->tiles_host.size() && std::equal(t.begin(), t.end(), c->tiles_host.begin(),
+                                                      [](const TileXY& a, const TileXY& b) { return a.x == b.x && a.y == b.y; }))
+        return RMR_OK;
+    if (t.size() > c->tiles_cap) {
+        if (c->d_tiles) (void)hipFree(c->d_tiles);
+        c->d_tiles = nullptr;
+        HIPCHK(c, hipMalloc((void**)&c->d_tiles, std::max<size_t>(1, t.size()) * sizeof(TileXY)));
+        c->tiles_cap = t.size();
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(c->d_tiles, t.data(), t.size() * sizeof(TileXY), hipMemcpyHostToDevice));
+    c->tiles_host = t;
+    return RMR_OK;
+}
+
+EventPair get_events(rmr_ctx* c) {
+    if (!c->pool.empty()) {
+        EventPair e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    EventPair e;
+    (void)hipEventCreate(&e.a);
+    (void)hipEventCreate(&e.b);
+    (void)hipEventCreate(&e.c);
+    return e;
+}
+
+int collect_timing(rmr_ctx* c) {
+    for (auto& e : c->pending) {
+        HIPCHK(c, hipEventSynchronize(e.c));
+        float t1 = 0, t2 = 0;
+        (void)hipEventElapsedTime(&t1, e.a, e.b);
+        (void)hipEventElapsedTime(&t2, e.b, e.c);
+        c->stats.trace_ms += t1;
+        c->stats.fold_ms += t2;
+        c->pool.push_back(e);
+    }
+    c->pending.clear();
+    return RMR_OK;
+}
+
+// Core: nspp samples over an 8x8 tile list, clipped to [x0,x1)x[y0,y1).
+int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, int x1, int y1,
+                 const float* times, uint32_t first_sample, uint32_t nspp) {
+    if (!c->scene_loaded) return fail(c, RMR_E_STATE, "no scene loaded (call rmr_load_scene_json / rmr_load_builtin_scene)");
+    if (c->params.use_env_tex) return fail(c, RMR_E_UNSUPPORTED, "useEnvTex != 0 is not supported");
+    if (tiles.empty() || nspp == 0) return RMR_OK;
+    if (!c->view_set) default_view(c);
+    int r;
+    if ((r = set_tiles(c, tiles))) return r;
+    const size_t plane = tiles.size() * 64;
+    size_t chunk = std::max<size_t>(1, c->samp_budget / (plane * sizeof(float4)));
+    chunk = std::min<size_t>(chunk, nspp);
+    if ((r = ensure_samp(c, plane * chunk))) return r;
+    if (nspp > c->times_cap) {
+        if (c->d_times) (void)hipFree(c->d_times);
+        c->d_times = nullptr;
+        HIPCHK(c, hipMalloc((void**)&c->d_times, nspp * sizeof(float)));
+        c->times_cap = nspp;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_times, times, nspp * sizeof(float), hipMemcpyHostToDevice, c->stream));
+
+    const CompiledScene& s = c->scene;
+    KParams P{};
+    P.prims = c->d_prims; P.ops = c->d_ops; P.consts = c->d_consts; P.mats = c->d_mats;
+    P.spec = c->d_spec; P.rm2 = c->d_rm2;
+    P.n_prims = (int)s.prims.size();
+    P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
+    P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
+    P.spec_sky = s.spectral_sky;
+    for (int i = 0; i < 3; i++) { P.sky[i] = s.sky[i]; P.rm2_light[i] = s.rm2.light_pos[i]; }
+    P.rm2_light_power = s.rm2.light_power;
+    P.rm2_node_id = s.rm2.node_mat_id;
+    P.max_dist = c->params.max_dist; P.step_mult = c->params.step_multiply;
+    P.max_steps = c->params.max_steps; P.max_bounces = c->params.max_bounces;
+    P.separate_channels = c->params.separate_channels;
+    for (int i = 0; i < 3; i++) {
+        P.eye[i] = c->view[i]; P.r00[i] = c->view[3 + i]; P.r01[i] = c->view[6 + i];
+        P.r10[i] = c->view[9 + i]; P.r11[i] = c->view[12 + i];
+    }
+    P.W = c->W; P.H = c->H;
+    P.x0 = x0; P.y0 = y0; P.x1 = x1; P.y1 = y1;
+    P.tiles = c->d_tiles;
+    P.n_tiles = (int)tiles.size();
+    P.samp = c->d_samp;
+    P.accum = c->d_accum;
+    P.queue = c->d_queue;
+    P.counters = c->d_counters;
+    P.shade_threshold = c->shade_threshold;
+
+    int bpc = c->grid_per_cu;
+    if (bpc <= 0) {
+        if (rmr::trace_occupancy(s.variant, &bpc) != 0 || bpc <= 0) bpc = 4;
+    }
+    const int grid = c->n_cu * bpc;
+    for (uint32_t k0 = 0; k0 < nspp; k0 += (uint32_t)chunk) {
+        const uint32_t n = (uint32_t)std::min<size_t>(chunk, nspp - k0);
+        P.nspp = n;
+        P.first_sample = first_sample + k0;
+        P.times = c->d_times + k0;
+        P.n_units = (uint64_t)n * plane;
+        HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(unsigned long long), c->stream));
+        EventPair ev = get_events(c);
+        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        HIPCHK(c, rmr::launch_trace(P, s.variant, c->kernel_mode == 0, grid, c->stream));
+        HIPCHK(c, hipEventRecord(ev.b, c->stream));
+        HIPCHK(c, rmr::launch_fold(P, c->stream));
+        HIPCHK(c, hipEventRecord(ev.c, c->stream));
+        c->pending.push_back(ev);
+        c->stats.trace_launches++;
+        c->stats.samples += (uint64_t)n * plane;  // upper bound; exact count below
+    }
+    return RMR_OK;
+}
+
+std::vector<TileXY> rect_tiles(int x0, int y0, int x1, int y1) {
+    std::vector<TileXY> t;
+    for (int y = y0; y < y1; y += 8)
+        for (int x = x0; x < x1; x += 8) t.push_back(TileXY{x, y});
+    return t;
+}
+
+int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+}  // namespace
+
+extern "C" {
+
+const char* rmr_build_info(void) {
+    return "rmr gfx950 (CDNA4): variants RM1/RM2/RM3; wave64 persistent path-state kernel; "
+           "scalar-cached scene tables; -ffp-contract=off deterministic math";
+}
+
+void rmr_default_params(rmr_params* p) {
+    if (!p) return;
+    p->max_dist = 1000.0f;  // Graphics.cpp:326
+    p->max_steps = 512;     // Graphics.cpp:327
+    p->max_bounces = 16;    // Graphics.cpp:328
+    p->step_multiply = 0.5f;  // Graphics.cpp:329
+    p->separate_channels = 0; // Graphics.cpp:340
+    p->use_env_tex = 0;       // Graphics.cpp:338
+}
+
+int rmr_create(rmr_ctx** out, int device) {
+    if (!out) return RMR_E_INVALID;
+    *out = nullptr;
+    rmr_ctx* c = new (std::nothrow) rmr_ctx();
+    if (!c) return RMR_E_NOMEM;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+        delete c;
+        return RMR_E_HIP;
+    }
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) { delete c; return RMR_E_HIP; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RMR_E_HIP; }
+    c->own_stream = true;
+    rmr_default_params(&c->params);
+    if (hipMalloc((void**)&c->d_queue, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        rmr_destroy(c);
+        return RMR_E_HIP;
+    }
+    if (const char* e = std::getenv("RMR_SHADE_T")) c->shade_threshold = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
+    if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
+    *out = c;
+    return RMR_OK;
+}
+
+void rmr_destroy(rmr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->pending) c->pool.push_back(e);
+    for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
+    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_samp,
+                    c->d_tiles, c->d_times, c->d_queue, c->d_counters};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rmr_last_error(const rmr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int rmr_set_stream(rmr_ctx* c, void* s) {
+    if (!c) return RMR_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    if (s) {
+        c->stream = (hipStream_t)s;
+        c->own_stream = false;
+    } else {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return RMR_OK;
+}
+
+int rmr_set_image_size(rmr_ctx* c, int w, int h) {
+    if (!c) return RMR_E_INVALID;
+    if (w <= 0 || h <= 0 || w > 32768 || h > 32768) return fail(c, RMR_E_INVALID, "bad image size");
+    c->pend_W = w;
+    c->pend_H = h;
+    return RMR_OK;
+}
+
+int rmr_get_image_size(const rmr_ctx* c, int* w, int* h) {
+    if (!c || !w || !h) return RMR_E_INVALID;
+    *w = c->W;
+    *h = c->H;
+    return RMR_OK;
+}
+
+int rmr_set_params(rmr_ctx* c, const rmr_params* p) {
+    if (!c || !p) return RMR_E_INVALID;
+    if (p->max_steps < 0 || p->max_bounces < 0 || !(p->max_dist > 0.0f)) return fail(c, RMR_E_INVALID, "bad params");
+    c->params = *p;
+    return RMR_OK;
+}
+
+int rmr_get_params(const rmr_ctx* c, rmr_params* p) {
+    if (!c || !p) return RMR_E_INVALID;
+    *p = c->params;
+    return RMR_OK;
+}
+
+int rmr_set_view(rmr_ctx* c, const float eye[3], const float r00[3], const float r01[3], const float r10[3],
+                 const float r11[3]) {
+    if (!c || !eye || !r00 || !r01 || !r10 || !r11) return RMR_E_INVALID;
+    for (int i = 0; i < 3; i++) {
+        c->view[i] = eye[i]; c->view[3 + i] = r00[i]; c->view[6 + i] = r01[i];
+        c->view[9 + i] = r10[i]; c->view[12 + i] = r11[i];
+    }
+    c->view_set = true;
+    return RMR_OK;
+}
+
+int rmr_load_scene_json(rmr_ctx* c, int variant, const char* json, size_t len) {
+    if (!c || !json) return RMR_E_INVALID;
+    try {
+        CompiledScene s = rmr::compile_scene(std::string(json, len), variant);
+        int r = validate_scene(c, s);
+        if (r) return r;
+        c->scene = std::move(s);
+    } catch (const rmr::SceneError& e) {
+        return fail(c, RMR_E_SCENE, e.what());
+    } catch (const std::exception& e) {
+        return fail(c, RMR_E_SCENE, e.what());
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    return upload_scene(c);
+}
+
+int rmr_load_scene_tables(rmr_ctx* c, const rmr_scene* s) {
+    if (!c || !s) return RMR_E_INVALID;
+    if (s->variant < RMR_VARIANT_RM1 || s->variant > RMR_VARIANT_RM3) return fail(c, RMR_E_INVALID, "bad variant");
+    if (s->n_prims < 0 || s->n_prims > RMR_MAX_PRIMS || s->n_ops < 0 || s->n_ops > RMR_MAX_OPS ||
+        s->n_consts < 0 || s->n_consts > RMR_MAX_CONSTS || s->n_materials < 0 || s->n_materials > RMR_MAX_MATERIALS)
+        return fail(c, RMR_E_INVALID, "table sizes out of range");
+    CompiledScene cs;
+    cs.from_tables(*s);
+    int r = validate_scene(c, cs);
+    if (r) return r;
+    c->scene = std::move(cs);
+    HIPCHK(c, hipSetDevice(c->device));
+    return upload_scene(c);
+}
+
+int rmr_load_builtin_scene(rmr_ctx* c, int variant) {
+    if (!c) return RMR_E_INVALID;
+    if (variant == RMR_VARIANT_RM2) return fail(c, RMR_E_SCENE, "RayMarch2.glsl needs a v2 scene for mat_func_1; use rmr_load_scene_json");
+    try {
+        c->scene = rmr::builtin_scene(variant);
+    } catch (const std::exception& e) {
+        return fail(c, RMR_E_SCENE, e.what());
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    return upload_scene(c);
+}
+
+int rmr_reload(rmr_ctx* c) {
+    if (!c) return RMR_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->accum_external && (c->pend_W != c->W || c->pend_H != c->H))
+        return fail(c, RMR_E_STATE, "bound accumulator cannot be resized");
+    const bool resize = (c->pend_W != c->W || c->pend_H != c->H);
+    c->W = c->pend_W;
+    c->H = c->pend_H;
+    if (resize) {
+        if (c->view_set) { /* caller's view is kept (reference: camera.calculateRays after Reload) */ }
+        int r = alloc_accum(c);
+        if (r) return r;
+    } else {
+        HIPCHK(c, hipMemsetAsync(c->d_accum, 0, (size_t)c->W * c->H * sizeof(float4), c->stream));
+    }
+    return RMR_OK;
+}
+
+int rmr_render(rmr_ctx* c, float time, float min_x, float min_y, float max_x, float max_y, uint32_t current_sample) {
+    if (!c) return RMR_E_INVALID;
+    // pix >= bounds.xy && pix < bounds.zw for integer pix (RM1:572) <=> pix in [ceil(min), ceil(max))
+    const int x0 = clampi((int)std::ceil(min_x), 0, c->W), y0 = clampi((int)std::ceil(min_y), 0, c->H);
+    const int x1 = clampi((int)std::ceil(max_x), 0, c->W), y1 = clampi((int)std::ceil(max_y), 0, c->H);
+    if (x1 <= x0 || y1 <= y0) return RMR_OK;
+    return render_tiles(c, rect_tiles(x0, y0, x1, y1), x0, y0, x1, y1, &time, current_sample, 1);
+}
+
+int rmr_render_spp(rmr_ctx* c, const float* times, int x0, int y0, int x1, int y1, uint32_t first_sample, uint32_t nspp) {
+    if (!c || (!times && nspp)) return RMR_E_INVALID;
+    x0 = clampi(x0, 0, c->W); x1 = clampi(x1, 0, c->W);
+    y0 = clampi(y0, 0, c->H); y1 = clampi(y1, 0, c->H);
+    if (x1 <= x0 || y1 <= y0) return RMR_OK;
+    return render_tiles(c, rect_tiles(x0, y0, x1, y1), x0, y0, x1, y1, times, first_sample, nspp);
+}
+
+int rmr_render_tiles(rmr_ctx* c, const float* times, const int32_t* tiles_xy, int n_tiles, int tile_size,
+                     uint32_t first_sample, uint32_t nspp) {
+    if (!c || (!times && nspp) || (!tiles_xy && n_tiles) || tile_size <= 0 || (tile_size % 8) != 0)
+        return fail(c, RMR_E_INVALID, "tile_size must be a positive multiple of 8");
+    std::vector<TileXY> t;
+    t.reserve((size_t)n_tiles * (tile_size / 8) * (tile_size / 8));
+    for (int i = 0; i < n_tiles; i++) {
+        const int bx = tiles_xy[2 * i] * tile_size, by = tiles_xy[2 * i + 1] * tile_size;
+        for (int y = by; y < std::min(by + tile_size, c->H); y += 8)
+            for (int x = bx; x < std::min(bx + tile_size, c->W); x += 8) t.push_back(TileXY{x, y});
+    }
+    if (t.empty()) return RMR_OK;
+    return render_tiles(c, t, 0, 0, c->W, c->H, times, first_sample, nspp);
+}
+
+int rmr_read_accum(rmr_ctx* c, float* rgba, size_t bytes) {
+    if (!c || !rgba) return RMR_E_INVALID;
+    const size_t need = (size_t)c->W * c->H * sizeof(float4);
+    if (bytes < need) return fail(c, RMR_E_INVALID, "buffer too small");
+    HIPCHK(c, hipMemcpyAsync(rgba, c->d_accum, need, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RMR_OK;
+}
+
+int rmr_write_accum(rmr_ctx* c, const float* rgba, size_t bytes) {
+    if (!c || !rgba) return RMR_E_INVALID;
+    const size_t need = (size_t)c->W * c->H * sizeof(float4);
+    if (bytes < need) return fail(c, RMR_E_INVALID, "buffer too small");
+    HIPCHK(c, hipMemcpyAsync(c->d_accum, rgba, need, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RMR_OK;
+}
+
+void* rmr_accum_device_ptr(rmr_ctx* c) { return c ? (void*)c->d_accum : nullptr; }
+
+int rmr_bind_accum(rmr_ctx* c, void* ptr, size_t bytes) {
+    if (!c || !ptr) return RMR_E_INVALID;
+    if (bytes < (size_t)c->W * c->H * sizeof(float4)) return fail(c, RMR_E_INVALID, "bound accumulator too small");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
+    c->d_accum = (float4*)ptr;
+    c->accum_external = true;
+    return RMR_OK;
+}
+
+int rmr_save_bmp(rmr_ctx* c, const char* path) {
+    if (!c || !path) return RMR_E_INVALID;
+    std::vector<float> host((size_t)c->W * c->H * 4);
+    int r = rmr_read_accum(c, host.data(), host.size() * sizeof(float));
+    if (r) return r;
+    r = rmr_encode_bmp(host.data(), c->W, c->H, path);
+    if (r) return fail(c, r, std::string("cannot write ") + path);
+    return RMR_OK;
+}
+
+int rmr_save_accum(rmr_ctx* c, const char* path, uint32_t samples_done) {
+    if (!c || !path) return RMR_E_INVALID;
+    std::vector<float> host((size_t)c->W * c->H * 4);
+    int r = rmr_read_accum(c, host.data(), host.size() * sizeof(float));
+    if (r) return r;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(c, RMR_E_IO, std::string("cannot open ") + path);
+    const char magic[8] = {'R', 'M', 'R', 'A', 'C', 'C', '1', 0};
+    const uint32_t hdr[3] = {(uint32_t)c->W, (uint32_t)c->H, samples_done};
+    bool ok = std::fwrite(magic, 1, 8, f) == 8 && std::fwrite(hdr, 4, 3, f) == 3 &&
+              std::fwrite(host.data(), sizeof(float), host.size(), f) == host.size();
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RMR_OK : fail(c, RMR_E_IO, "write failed");
+}
+
+int rmr_load_accum(rmr_ctx* c, const char* path, uint32_t* samples_done) {
+    if (!c || !path) return RMR_E_INVALID;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(c, RMR_E_IO, std::string("cannot open ") + path);
+    char magic[8];
+    uint32_t hdr[3];
+    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, "RMRACC1", 8) != 0 || std::fread(hdr, 4, 3, f) != 3) {
+        std::fclose(f);
+        return fail(c, RMR_E_IO, "not an rmr accumulator file");
+    }
+    if ((int)hdr[0] != c->W || (int)hdr[1] != c->H) {
+        std::fclose(f);
+        return fail(c, RMR_E_STATE, "accumulator size does not match the image size");
+    }
+    std::vector<float> host((size_t)c->W * c->H * 4);
+    const bool ok = std::fread(host.data(), sizeof(float), host.size(), f) == host.size();
+    std::fclose(f);
+    if (!ok) return fail(c, RMR_E_IO, "truncated accumulator file");
+    if (samples_done) *samples_done = hdr[2];
+    return rmr_write_accum(c, host.data(), host.size() * sizeof(float));
+}
+
+int rmr_sync(rmr_ctx* c) {
+    if (!c) return RMR_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return collect_timing(c);
+}
+
+int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
+    if (!c || !out) return RMR_E_INVALID;
+    int r = rmr_sync(c);
+    if (r) return r;
+    unsigned long long cnt[4];
+    HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+    c->stats.map_evals = cnt[0];
+    *out = c->stats;
+    return RMR_OK;
+}
+
+int rmr_reset_stats(rmr_ctx* c) {
+    if (!c) return RMR_E_INVALID;
+    int r = rmr_sync(c);
+    if (r) return r;
+    const double fpm = c->stats.flops_per_map;
+    c->stats = rmr_stats{};
+    c->stats.flops_per_map = fpm;
+    HIPCHK(c, hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)));
+    return RMR_OK;
+}
+
+int rmr_set_kernel(rmr_ctx* c, int kernel) {
+    if (!c || kernel < 0 || kernel > 1) return RMR_E_INVALID;
+    c->kernel_mode = kernel;
+    return RMR_OK;
+}
+
+int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long samp_budget_bytes) {
+    if (!c) return RMR_E_INVALID;
+    if (shade_threshold > 0) c->shade_threshold = std::min(64, shade_threshold);
+    if (grid_per_cu >= 0) c->grid_per_cu = grid_per_cu;
+    if (samp_budget_bytes > 0) c->samp_budget = (size_t)samp_budget_bytes;
+    return RMR_OK;
+}
+
+// Per-sample radiance planes for parity tests: out[k][y-y0][x-x0][4] for the rect.
+int rmr_trace_samples(rmr_ctx* c, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out) {
+    if (!c || !times || !out) return RMR_E_INVALID;
+    x0 = clampi(x0, 0, c->W); x1 = clampi(x1, 0, c->W);
+    y0 = clampi(y0, 0, c->H); y1 = clampi(y1, 0, c->H);
+    if (x1 <= x0 || y1 <= y0 || nspp == 0) return RMR_OK;
+    std::vector<TileXY> tiles = rect_tiles(x0, y0, x1, y1);
+    const size_t saved_budget = c->samp_budget;
+    const size_t plane = tiles.size() * 64;
+    c->samp_budget = std::max(saved_budget, plane * nspp * sizeof(float4));  // one chunk
+    // render into a scratch accumulator region: trace writes samp planes; fold into accum is harmless
+    std::vector<float> keep((size_t)c->W * c->H * 4);
+    int r = rmr_read_accum(c, keep.data(), keep.size() * sizeof(float));
+    if (!r) r = render_tiles(c, tiles, x0, y0, x1, y1, times, 0, nspp);
+    c->samp_budget = saved_budget;
+    if (r) return r;
+    std::vector<float4> h(plane * nspp);
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->d_samp, h.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int w = x1 - x0, hh = y1 - y0;
+    const int tx = (w + 7) / 8;
+    for (uint32_t k = 0; k < nspp; k++)
+        for (int y = 0; y < hh; y++)
+            for (int x = 0; x < w; x++) {
+                const size_t tile = (size_t)(y / 8) * tx + (x / 8);
+                const size_t lane = (size_t)(y % 8) * 8 + (x % 8);
+                const float4 v = h[(size_t)k * plane + tile * 64 + lane];
+                float* o = out + (((size_t)k * hh + y) * w + x) * 4;
+                o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+            }
+    return rmr_write_accum(c, keep.data(), keep.size() * sizeof(float));
+}
+
+int rmr_abi_sizes(int32_t* out, int n) {
+    const int32_t s[] = {(int32_t)sizeof(rmr_prim), (int32_t)sizeof(rmr_op), (int32_t)sizeof(rmr_material),
+                         (int32_t)sizeof(rmr_spectral), (int32_t)sizeof(rmr_rm2_consts), (int32_t)sizeof(rmr_scene),
+                         (int32_t)sizeof(rmr_params), (int32_t)sizeof(rmr_stats)};
+    const int m = (int)(sizeof s / sizeof s[0]);
+    for (int i = 0; i < n && i < m; i++) out[i] = s[i];
+    return m;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+// rmr_internal.h — kernel launch parameters shared by the host API (rmr_api.cpp) and the kernels.
+#pragma once
+#include <stdint.h>
+#include "../../include/rmr_tables.h"
+
+namespace rmr {
+
+// One 8x8 pixel tile = one wave's initial 64 paths (the reference RM1 workgroup shape,
+// RayMarch.glsl:11). tiles[] holds the tile origin (x, y) in pixels.
+struct TileXY { int32_t x, y; };
+
+struct KParams {
+    // ---- scene tables (device pointers, read-only) ----
+    const rmr_prim* prims;
+    const rmr_op* ops;
+    const float* consts;
+    const rmr_material* mats;
+    const rmr_spectral* spec;
+    const rmr_rm2_consts* rm2;
+    int32_t n_prims;
+    int32_t n_mats;
+    int32_t v2_begin, v2_end;
+    rmr_spectral spec_sky;
+    float sky[3];
+    float rm2_light[3];
+    float rm2_light_power;
+    int32_t rm2_node_id;
+    // ---- render parameters (Graphics::Render uniforms) ----
+    float max_dist, step_mult;
+    int32_t max_steps, max_bounces, separate_channels;
+    // ---- view (setView uniforms, shader order) ----
+    float eye[3], r00[3], r01[3], r10[3], r11[3];
+    int32_t W, H;
+    // ---- work ----
+    int32_t x0, y0, x1, y1;     // clip rect (pixels inside = rendered)
+    const TileXY* tiles;        // n_tiles tiles
+    int32_t n_tiles;
+    uint32_t nspp;              // samples in this launch
+    uint32_t first_sample;      // running-mean index of sample 0
+    const float* times;         // [nspp] rand() seed per sample
+    uint64_t n_units;           // nspp * n_tiles * 64
+    float4* samp;               // [nspp][n_tiles][64] per-sample radiance
+    float4* accum;              // W*H running mean
+    unsigned long long* queue;  // persistent work counter
+    unsigned long long* counters; // [0] map evals, [1] samples traced
+    int32_t shade_threshold;    // deferred-shading batch size (lanes)
+};
+
+}  // namespace rmr

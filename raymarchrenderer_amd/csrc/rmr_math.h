@@ -1,0 +1,206 @@
+// rmr_math.h — gfx950 device math for the rmr kernels.
+//
+// Float semantics (shared *by definition* with the CPU oracle, oracle/detmath.h; compiled with
+// -ffp-contract=off so that only the fmaf calls below fuse):
+//   dot(a,b) = fma(a.x,b.x, fma(a.y,b.y, a.z*b.z));  normalize(a) = a * (1/length(a));
+//   mix(x,y,a) = fma(a, y-x, x);  mod(x,y) = fma(-y, floor(x/y), x);  mat3*v fused column sum;
+//   sin/cos: Cody-Waite pi/2 reduction + minimax polynomials; acos: FreeBSD acosf rational form.
+// sqrt and '/' are the correctly rounded IEEE operations (hipcc's default lowering), which is what
+// makes a bit-exact CPU restatement possible.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rmr {
+
+struct V2 { float x, y; };
+struct V3 { float x, y, z; };
+
+#define RMR_D __device__ __forceinline__
+
+RMR_D V2 v2(float x, float y) { return V2{x, y}; }
+RMR_D V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+RMR_D V3 v3s(float s) { return V3{s, s, s}; }
+RMR_D V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RMR_D V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RMR_D V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RMR_D V3 operator/(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }
+RMR_D V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+RMR_D V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+RMR_D V3 vabs(V3 a) { return v3(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+RMR_D V3 vmax0(V3 a) { return v3(fmaxf(a.x, 0.0f), fmaxf(a.y, 0.0f), fmaxf(a.z, 0.0f)); }
+RMR_D V3 vmin(V3 a, V3 b) { return v3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+RMR_D V3 vmax(V3 a, V3 b) { return v3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+RMR_D bool is_zero(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+RMR_D bool veq(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+RMR_D float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+RMR_D float dot2(V2 a, V2 b) { return fmaf(a.x, b.x, a.y * b.y); }
+RMR_D float length(V3 a) { return sqrtf(dot(a, a)); }
+RMR_D V3 normalize(V3 a) { float inv = 1.0f / length(a); return a * inv; }
+RMR_D V3 vfma(V3 a, float s, V3 b) { return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z)); }
+RMR_D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+RMR_D float fmix(float x, float y, float a) { return fmaf(a, y - x, x); }
+RMR_D V3 vmix(V3 x, V3 y, float a) { return v3(fmix(x.x, y.x, a), fmix(x.y, y.y, a), fmix(x.z, y.z, a)); }
+RMR_D V3 mat_mul(V3 c0, V3 c1, V3 c2, V3 v) {
+    return v3(fmaf(c0.x, v.x, fmaf(c1.x, v.y, c2.x * v.z)),
+              fmaf(c0.y, v.x, fmaf(c1.y, v.y, c2.y * v.z)),
+              fmaf(c0.z, v.x, fmaf(c1.z, v.y, c2.z * v.z)));
+}
+RMR_D float clampf(float x, float a, float b) { return fminf(fmaxf(x, a), b); }
+RMR_D float fractf(float x) { return x - floorf(x); }
+RMR_D float modf_glsl(float x, float y) { return fmaf(-y, floorf(x / y), x); }
+RMR_D V3 reflect(V3 I, V3 N) { float k = 2.0f * dot(N, I); return vfma(N, -k, I); }
+RMR_D V3 refract(V3 I, V3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return v3s(0.0f);
+    float m = eta * d + sqrtf(k);
+    return v3(eta * I.x - m * N.x, eta * I.y - m * N.y, eta * I.z - m * N.z);
+}
+RMR_D float pow2(float x) { return x * x; }
+RMR_D float pow5(float x) { float x2 = x * x; return (x2 * x2) * x; }
+
+// ---- sin / cos -----------------------------------------------------------------------------
+RMR_D float sin_poly(float r, float s) {
+    float p = fmaf(s, -1.9515295891e-4f, 8.3321608736e-3f);
+    p = fmaf(s, p, -1.6666654611e-1f);
+    return fmaf(r * s, p, r);
+}
+RMR_D float cos_poly(float s) {
+    float p = fmaf(s, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    p = fmaf(s, p, 4.166664568298827e-2f);
+    float t = fmaf(s, -0.5f, 1.0f);
+    return fmaf(s * s, p, t);
+}
+RMR_D float reduce_pio2(float x, int& q) {
+    float k = rintf(x * 0.636619772367581343f);
+    k = fminf(fmaxf(k, -8388608.0f), 8388608.0f);
+    float r = fmaf(-k, 1.57079637050628662109375f, x);
+    r = fmaf(-k, -4.37113882867379e-08f, r);
+    r = fmaf(-k, -1.71512451e-15f, r);
+    q = ((int)k) & 3;
+    return r;
+}
+RMR_D float det_sin(float x) {
+    int q; float r = reduce_pio2(x, q); float s = r * r;
+    float v = (q & 1) ? cos_poly(s) : sin_poly(r, s);
+    return (q & 2) ? -v : v;
+}
+RMR_D float det_cos(float x) {
+    int q; float r = reduce_pio2(x, q); float s = r * r;
+    float v = (q & 1) ? sin_poly(r, s) : cos_poly(s);
+    return ((q + 1) & 2) ? -v : v;
+}
+// sin and cos of one argument (one reduction)
+RMR_D void det_sincos(float x, float& sv, float& cv) {
+    int q; float r = reduce_pio2(x, q); float s = r * r;
+    float sp = sin_poly(r, s), cp = cos_poly(s);
+    float a = (q & 1) ? cp : sp;
+    float b = (q & 1) ? sp : cp;
+    sv = (q & 2) ? -a : a;
+    cv = ((q + 1) & 2) ? -b : b;
+}
+
+// ---- acos (FreeBSD acosf) -------------------------------------------------------------------
+RMR_D float acos_R(float z) {
+    float p = z * (1.6666586697e-01f + z * (-4.2743422091e-02f + z * -8.6563630030e-03f));
+    float q = 1.0f + z * -7.0662963390e-01f;
+    return p / q;
+}
+RMR_D float det_acos(float x) {
+    const float pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+    uint32_t hx = __float_as_uint(x), ix = hx & 0x7fffffffu;
+    if (ix >= 0x3f800000u) {
+        if (ix == 0x3f800000u) return (hx >> 31) ? 3.14159274101257324219f : 0.0f;
+        return __uint_as_float(0x7fc00000u);
+    }
+    if (ix < 0x3f000000u) {
+        if (ix <= 0x32800000u) return 1.57079637050628662109375f;
+        return pio2_hi - (x - (pio2_lo - x * acos_R(x * x)));
+    }
+    if (hx >> 31) {
+        float z = (1.0f + x) * 0.5f;
+        float s = sqrtf(z);
+        float w = acos_R(z) * s - pio2_lo;
+        return 2.0f * (pio2_hi - (s + w));
+    }
+    float z = (1.0f - x) * 0.5f;
+    float s = sqrtf(z);
+    float df = __uint_as_float(__float_as_uint(s) & 0xfffff000u);
+    float c = (z - df * df) / (s + df);
+    float w = acos_R(z) * s + c;
+    return 2.0f * (df + w);
+}
+
+// ---- log / exp / pow / atan2 (Mandelbulb) ---------------------------------------------------
+RMR_D float det_log(float x) {
+    if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_huge_valf() : __uint_as_float(0x7fc00000u);
+    if (x == __builtin_huge_valf()) return x;
+    uint32_t u = __float_as_uint(x);
+    int e = 0;
+    if (u < 0x00800000u) { x = x * 16777216.0f; u = __float_as_uint(x); e = -24; }
+    u += 0x3f800000u - 0x3f3504f3u;
+    e += (int)(u >> 23) - 0x7f;
+    u = (u & 0x007fffffu) + 0x3f3504f3u;
+    float m = __uint_as_float(u);
+    float f = m - 1.0f;
+    float s = f / (2.0f + f);
+    float z = s * s;
+    float w = z * z;
+    float t1 = w * fmaf(w, 0.24279078841f, 0.40000972152f);
+    float t2 = z * fmaf(w, 0.28498786688f, 0.66666662693f);
+    float R = t2 + t1;
+    float hfsq = 0.5f * f * f;
+    float dk = (float)e;
+    return fmaf(dk, 6.9313812256e-01f, -((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f));
+}
+RMR_D float det_exp(float x) {
+    if (x > 88.7f) return __builtin_huge_valf();
+    if (x < -103.0f) return 0.0f;
+    if (x != x) return x;
+    float k = rintf(x * 1.44269504089f);
+    float r = fmaf(-k, 6.93145752e-1f, x);
+    r = fmaf(-k, 1.42860677e-6f, r);
+    float p = fmaf(r, 1.9875691500e-4f, 1.3981999507e-3f);
+    p = fmaf(r, p, 8.3334519073e-3f);
+    p = fmaf(r, p, 4.1665795894e-2f);
+    p = fmaf(r, p, 1.6666665459e-1f);
+    p = fmaf(r, p, 5.0000001201e-1f);
+    float e = fmaf(r * r, p, r) + 1.0f;
+    int ki = (int)k;
+    int k1 = ki / 2, k2 = ki - k1;
+    return (e * __uint_as_float((uint32_t)(k1 + 127) << 23)) * __uint_as_float((uint32_t)(k2 + 127) << 23);
+}
+RMR_D float det_pow(float x, float y) {
+    if (y == 0.0f) return 1.0f;
+    if (x == 0.0f) return 0.0f;
+    return det_exp(y * det_log(x));
+}
+RMR_D float det_atan(float x) {
+    float a = fabsf(x);
+    bool inv = a > 1.0f;
+    float t = inv ? 1.0f / a : a;
+    float s = t * t;
+    float p = fmaf(s, -0.0117212f, 0.05265332f);
+    p = fmaf(s, p, -0.11643287f);
+    p = fmaf(s, p, 0.19354346f);
+    p = fmaf(s, p, -0.33262347f);
+    p = fmaf(s, p, 0.99997726f);
+    float r = t * p;
+    if (inv) r = 1.57079637050628662109375f - r;
+    return (x < 0.0f) ? -r : r;
+}
+RMR_D float det_atan2(float y, float x) {
+    if (x == 0.0f && y == 0.0f) return 0.0f;
+    float r;
+    if (fabsf(x) >= fabsf(y)) {
+        r = det_atan(y / x);
+        if (x < 0.0f) r = (y < 0.0f) ? r - 3.14159274101257324219f : r + 3.14159274101257324219f;
+    } else {
+        r = det_atan(x / y);
+        r = ((y < 0.0f) ? -1.57079637050628662109375f : 1.57079637050628662109375f) - r;
+    }
+    return r;
+}
+
+}  // namespace rmr
