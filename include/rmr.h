@@ -52,6 +52,8 @@ typedef struct rmr_stats {
     double   trace_ms;       /* summed trace-kernel time measured with HIP events              */
     double   fold_ms;        /* summed accumulate-kernel time                                  */
     double   flops_per_map;  /* algorithmic flops of one map() for the loaded scene            */
+    uint64_t map_iters;      /* wave-level map() iterations: map_evals/(64*map_iters) = lane use */
+    uint64_t shade_batches;  /* wave-level deferred-shading batches                             */
 } rmr_stats;
 
 /* ---- lifetime --------------------------------------------------------------------------- */

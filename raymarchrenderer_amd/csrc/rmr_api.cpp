@@ -22,9 +22,9 @@
 #include "scene.hpp"
 
 namespace rmr {
-hipError_t launch_trace(const KParams& P, int variant, bool persistent, int grid, hipStream_t s);
+hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool persistent, int grid, hipStream_t s);
 hipError_t launch_fold(const KParams& P, hipStream_t s);
-int trace_occupancy(int variant, int* blocks_per_cu);
+int trace_occupancy(int variant, int np, bool prog, int* blocks_per_cu);
 }  // namespace rmr
 
 using rmr::CompiledScene;
@@ -52,6 +52,10 @@ struct rmr_ctx {
     rmr_material* d_mats = nullptr;
     rmr_spectral* d_spec = nullptr;
     rmr_rm2_consts* d_rm2 = nullptr;
+    rmr::DPrim* d_dprims = nullptr;
+    rmr::DMat* d_dmats = nullptr;
+    int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
+    bool has_prog = true;  // RM1 scene has materials needing the generic node interpreter
     // buffers
     float4* d_accum = nullptr;
     bool accum_external = false;
@@ -68,7 +72,7 @@ struct rmr_ctx {
     std::vector<EventPair> pending, pool;
     rmr_stats stats{};
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
-    int shade_threshold = 24;
+    int shade_threshold = 10;
     int grid_per_cu = 0;  // 0 = occupancy
     size_t samp_budget = (size_t)8 << 30;
     std::string err;
@@ -124,6 +128,49 @@ int upload_scene(rmr_ctx* c) {
     if ((r = dev_upload(c, &c->d_mats, s.materials.data(), s.materials.size()))) return r;
     if ((r = dev_upload(c, &c->d_spec, s.spectral.data(), s.spectral.size()))) return r;
     if ((r = dev_upload(c, &c->d_rm2, &s.rm2, 1))) return r;
+    // packed prims + map() specialisation
+    bool simple = true;
+    for (const auto& p : s.prims) simple = simple && (p.type == RMR_PRIM_SPHERE || p.type == RMR_PRIM_BOX);
+    const size_t n = s.prims.size();
+    c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : 0));
+    std::vector<rmr::DPrim> dp(std::max<size_t>(n, 8));
+    for (size_t i = 0; i < dp.size(); i++) {
+        rmr::DPrim q{};
+        if (i < n) {
+            const rmr_prim& p = s.prims[i];
+            for (int k = 0; k < 3; k++) { q.c[k] = p.c[k]; q.r[k] = p.r[k]; }
+            q.type = p.type;
+            q.mat_id = p.mat_id;
+        }
+        dp[i] = q;
+    }
+    if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
+    // shading kinds (RM1): recognise the single-node diffuse / emission materials
+    std::vector<rmr::DMat> dm(std::max<size_t>(1, s.materials.size()));
+    for (size_t i = 0; i < s.materials.size(); i++) {
+        const rmr_material& m = s.materials[i];
+        rmr::DMat d{};
+        d.kind = m.defined ? rmr::MAT_PROGRAM : rmr::MAT_NONE;
+        if (m.defined && m.prog_end - m.prog_begin == 1 && m.inside_var < 0 && m.hit_var < 0) {
+            const rmr_op& op = s.ops[(size_t)m.prog_begin];
+            auto lit = [&](int ref, float* out) {
+                if (!RMR_OPND_IS_CONST(ref)) return false;
+                const int k = RMR_OPND_CONST_INDEX(ref);
+                for (int j = 0; j < 3; j++) out[j] = s.consts[3 * (size_t)k + j];
+                return true;
+            };
+            if (op.code == RMR_OP_M_DIFFUSE && m.color_var == op.out[0] && m.dir_var == op.out[1] &&
+                op.out[0] != op.out[1] && lit(op.in[0], d.c))
+                d.kind = rmr::MAT_DIFFUSE;
+            else if (op.code == RMR_OP_M_EMISSION && m.color_var == op.out[0] && m.dir_var < 0 &&
+                     lit(op.in[0], d.c) && lit(op.in[1], d.p))
+                d.kind = rmr::MAT_EMISSION;
+        }
+        dm[i] = d;
+    }
+    c->has_prog = false;
+    for (const auto& d : dm) c->has_prog = c->has_prog || d.kind == rmr::MAT_PROGRAM;
+    if ((r = dev_upload(c, &c->d_dmats, dm.data(), dm.size()))) return r;
     c->scene_loaded = true;
     c->stats.flops_per_map = s.flops_per_map();
     return RMR_OK;
@@ -235,6 +282,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     KParams P{};
     P.prims = c->d_prims; P.ops = c->d_ops; P.consts = c->d_consts; P.mats = c->d_mats;
     P.spec = c->d_spec; P.rm2 = c->d_rm2;
+    P.dprims = c->d_dprims; P.dmats = c->d_dmats;
     P.n_prims = (int)s.prims.size();
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
@@ -261,7 +309,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
 
     int bpc = c->grid_per_cu;
     if (bpc <= 0) {
-        if (rmr::trace_occupancy(s.variant, &bpc) != 0 || bpc <= 0) bpc = 4;
+        if (rmr::trace_occupancy(s.variant, c->map_np, c->has_prog, &bpc) != 0 || bpc <= 0) bpc = 4;
     }
     const int grid = c->n_cu * bpc;
     for (uint32_t k0 = 0; k0 < nspp; k0 += (uint32_t)chunk) {
@@ -273,7 +321,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(unsigned long long), c->stream));
         EventPair ev = get_events(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
-        HIPCHK(c, rmr::launch_trace(P, s.variant, c->kernel_mode == 0, grid, c->stream));
+        HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         HIPCHK(c, rmr::launch_fold(P, c->stream));
         HIPCHK(c, hipEventRecord(ev.c, c->stream));
@@ -348,7 +396,7 @@ void rmr_destroy(rmr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
-    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_samp,
+    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_samp,
                     c->d_tiles, c->d_times, c->d_queue, c->d_counters};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -595,6 +643,8 @@ int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
     unsigned long long cnt[4];
     HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
     c->stats.map_evals = cnt[0];
+    c->stats.map_iters = cnt[1];
+    c->stats.shade_batches = cnt[2];
     *out = c->stats;
     return RMR_OK;
 }

@@ -9,6 +9,28 @@ namespace rmr {
 // RayMarch.glsl:11). tiles[] holds the tile origin (x, y) in pixels.
 struct TileXY { int32_t x, y; };
 
+// Packed primitive for the sphere/box fast paths: one s_load_dwordx8 per prim.
+struct DPrim {
+    float c[3];
+    float r[3];
+    int32_t type;  // RMR_PRIM_SPHERE / RMR_PRIM_BOX; 0 = padding (never evaluated)
+    float mat_id;
+};
+
+// Material shading kind, precomputed on the host from the v1 node program (rmr_material).
+enum MatKind : int32_t {
+    MAT_NONE = 0,      // no `case` for this id: outputs stay vec3(0) -> path ends black
+    MAT_DIFFUSE = 1,   // single shader_diffuse(literal) node, color/dir wired straight out
+    MAT_EMISSION = 2,  // single shader_emission(literal, literal) node, dir not written
+    MAT_PROGRAM = 3,   // anything else: the generic node interpreter
+};
+struct DMat {
+    int32_t kind;
+    float c[3];   // diffuse / emission color literal
+    float p[3];   // emission power literal
+    int32_t pad;
+};
+
 struct KParams {
     // ---- scene tables (device pointers, read-only) ----
     const rmr_prim* prims;
@@ -17,6 +39,8 @@ struct KParams {
     const rmr_material* mats;
     const rmr_spectral* spec;
     const rmr_rm2_consts* rm2;
+    const DPrim* dprims;        // packed prims (fast map paths)
+    const DMat* dmats;          // per-id shading kind (RM1)
     int32_t n_prims;
     int32_t n_mats;
     int32_t v2_begin, v2_end;

@@ -29,6 +29,7 @@ typedef const __attribute__((address_space(4))) rmr_prim CPrim;
 typedef const __attribute__((address_space(4))) rmr_op COp;
 typedef const __attribute__((address_space(4))) float CFloat;
 typedef const __attribute__((address_space(4))) rmr_material CMat;
+typedef const __attribute__((address_space(4))) DPrim CDPrim;
 
 #define PI_F 3.14159274101257324219f
 
@@ -180,7 +181,56 @@ __device__ __noinline__ float obj_program(const KParams& P, int begin, int end, 
 
 // map(p), RM1:224-231 + the //#OBJINSERT fold (Graphics.cpp:107-112): opU keeps the later object
 // on ties (RM1:219-222). The prim index is wave-uniform: every table read is a scalar load.
-RMR_D V2 scene_map(const KParams& P, V3 p) {
+//
+// NP > 0 : sphere/box scene padded to NP prims, loop fully unrolled -> all s_loads issue at the
+//          top of map() and one wait covers them;
+// NP == 0: sphere/box scene of any size, software-pipelined scalar loads (prim j+1 in flight
+//          while prim j is evaluated);
+// NP < 0 : general scene (node programs, Mandelbulb) through the 48-byte rmr_prim rows.
+RMR_D void opu(V2& d, float dj, float mid) {
+    const bool keep = d.x < dj;
+    d.x = keep ? d.x : dj;
+    d.y = keep ? d.y : mid;
+}
+
+template <int NP>
+RMR_D V2 map_fixed(const KParams& P, V3 p) {
+    CDPrim* pr = (CDPrim*)P.dprims;
+    V2 d = v2(P.max_dist, -1.0f);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int type = pr[j].type;
+        const V3 c = v3(pr[j].c[0], pr[j].c[1], pr[j].c[2]);
+        const V3 r = v3(pr[j].r[0], pr[j].r[1], pr[j].r[2]);
+        const float mid = pr[j].mat_id;
+        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
+    }
+    return d;
+}
+
+RMR_D V2 map_loop(const KParams& P, V3 p) {
+    CDPrim* pr = (CDPrim*)P.dprims;
+    V2 d = v2(P.max_dist, -1.0f);
+    const int n = P.n_prims;
+    int type = pr[0].type;
+    V3 c = v3(pr[0].c[0], pr[0].c[1], pr[0].c[2]);
+    V3 r = v3(pr[0].r[0], pr[0].r[1], pr[0].r[2]);
+    float mid = pr[0].mat_id;
+    for (int j = 0; j < n; ++j) {
+        const int jn = (j + 1 < n) ? j + 1 : j;
+        const int ntype = pr[jn].type;
+        const V3 nc = v3(pr[jn].c[0], pr[jn].c[1], pr[jn].c[2]);
+        const V3 nr = v3(pr[jn].r[0], pr[jn].r[1], pr[jn].r[2]);
+        const float nmid = pr[jn].mat_id;
+        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
+        type = ntype; c = nc; r = nr; mid = nmid;
+    }
+    return d;
+}
+
+RMR_D V2 map_general(const KParams& P, V3 p) {
     CPrim* pr = (CPrim*)P.prims;
     V2 d = v2(P.max_dist, -1.0f);
     const int n = P.n_prims;
@@ -193,12 +243,16 @@ RMR_D V2 scene_map(const KParams& P, V3 p) {
         else if (type == RMR_PRIM_SPHERE) dj = sd_sphere(p, c, r.x);
         else if (type == RMR_PRIM_MANDELBULB) dj = sd_mandelbulb(p, c, r);
         else dj = obj_program(P, pr[j].prog_begin, pr[j].prog_end, pr[j].dist_var, p);
-        const float mid = pr[j].mat_id;
-        const bool keep = d.x < dj;
-        d.x = keep ? d.x : dj;
-        d.y = keep ? d.y : mid;
+        opu(d, dj, pr[j].mat_id);
     }
     return d;
+}
+
+template <int NP>
+RMR_D V2 scene_map(const KParams& P, V3 p) {
+    if constexpr (NP > 0) return map_fixed<NP>(P, p);
+    else if constexpr (NP == 0) return map_loop(P, p);
+    else return map_general(P, p);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -618,24 +672,35 @@ RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) 
 // ------------------------------------------------------------------------------------------
 // shading of the parked lanes
 // ------------------------------------------------------------------------------------------
-template <int VAR>
+template <int VAR, bool PROG>
 RMR_D void shade(const KParams& P, Lane& L) {
     if (VAR == RMR_VARIANT_RM1) {
         const bool want = (L.phase == PH_HIT);
         const int id = want ? (int)L.mid : -1;
-        CMat* mats = (CMat*)P.mats;
-        bool valid = want && id >= 0 && id < P.n_mats;
-        if (valid) valid = P.mats[id].defined != 0;
-        V3 nc = v3s(0.0f), nd = v3s(0.0f), ni = v3s(0.0f), nh = v3s(0.0f);
-        uint64_t pending = __ballot(valid);
-        while (pending) {
-            const int lead = __ffsll((unsigned long long)pending) - 1;
-            const int m = __builtin_amdgcn_readlane(id, lead);
-            const bool mine = valid && id == m;
-            if (mine) run_material_v1(P, L, m, nc, nd, ni, nh);
-            pending &= ~__ballot(mine);
+        int kind = MAT_NONE;
+        DMat dm;
+        if (want && id >= 0 && id < P.n_mats) {
+            dm = P.dmats[id];
+            kind = dm.kind;
         }
-        (void)mats;
+        V3 nc = v3s(0.0f), nd = v3s(0.0f), ni = v3s(0.0f), nh = v3s(0.0f);
+        if (kind == MAT_DIFFUSE) {          // shader_diffuse(ray, c, color, dir), RM1:378-387
+            nc = v3(dm.c[0], dm.c[1], dm.c[2]);
+            nd = hemisphere(L, v2(L.hit.x, L.hit.y), v2(L.hit.z, L.hit.x), L.nrm);
+        } else if (kind == MAT_EMISSION) {  // shader_emission(ray, c, p, color), RM1:476-479
+            nc = v3(dm.c[0], dm.c[1], dm.c[2]) * gray_ch(v3(dm.p[0], dm.p[1], dm.p[2]) * channel_vec(L.chan), L.chan);
+        }
+        if constexpr (PROG) {  // generic node programs, one wave-uniform material at a time
+            const bool valid = (kind == MAT_PROGRAM);
+            uint64_t pending = __ballot(valid);
+            while (pending) {
+                const int lead = __ffsll((unsigned long long)pending) - 1;
+                const int m = __builtin_amdgcn_readlane(id, lead);
+                const bool mine = valid && id == m;
+                if (mine) run_material_v1(P, L, m, nc, nd, ni, nh);
+                pending &= ~__ballot(mine);
+            }
+        }
         if (want) rm1_after_material(P, L, nc, nd, ni, nh);
         if (L.phase == PH_MISS) {  // shader_emission(ray, skyColor(dir), vec3(1), emit), RM1:555-561
             const V3 emit = v3(P.sky[0], P.sky[1], P.sky[2]) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
@@ -732,11 +797,11 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 // ------------------------------------------------------------------------------------------
 // the trace kernel
 // ------------------------------------------------------------------------------------------
-template <int VAR, bool PERSIST>
+template <int VAR, int NP, bool PERSIST, bool PROG>
 __global__ __launch_bounds__(256) void k_trace(KParams P) {
     Lane L;
     L.phase = PH_IDLE;
-    uint64_t maps = 0;
+    uint64_t maps = 0, iters = 0, shades = 0;
     constexpr uint64_t CHUNK = 128;
     uint64_t rnext = 0, rend = 0;
     bool exhausted = false;
@@ -779,16 +844,18 @@ __global__ __launch_bounds__(256) void k_trace(KParams P) {
         if (amask) {
             if (act) {
                 const V3 p = (L.phase == PH_NORMAL) ? probe_point(L) : vfma(L.d, L.t, L.o);
-                const V2 m = scene_map(P, p);
+                const V2 m = scene_map<NP>(P, p);
                 if (L.phase == PH_NORMAL) normal_update(L, m.x);
                 else march_update(P, L, m);
             }
             maps += (uint64_t)__popcll(amask);
+            iters++;
         }
         const uint64_t smask = __ballot(is_shade(L.phase));
         const uint64_t amask2 = __ballot(is_active(L.phase));
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
-            if (is_shade(L.phase)) shade<VAR>(P, L);
+            shades++;
+            if (is_shade(L.phase)) shade<VAR, PROG>(P, L);
             if (L.phase == PH_DONE) {
                 P.samp[L.unit] = make_float4(L.acc.x, L.acc.y, L.acc.z, 1.0f);
                 L.phase = PH_IDLE;
@@ -802,7 +869,11 @@ __global__ __launch_bounds__(256) void k_trace(KParams P) {
         const uint64_t live = __ballot(L.phase != PH_IDLE);
         if (live == 0 && exhausted) break;
     }
-    if (__lane_id() == 0) atomicAdd(P.counters, (unsigned long long)maps);
+    if (__lane_id() == 0) {
+        atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
+        atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
+        atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
+    }
 }
 
 // Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
@@ -837,20 +908,33 @@ __global__ __launch_bounds__(256) void k_fold(KParams P) {
 
 // ---- host-side launchers (C++ linkage, used by rmr_api.cpp) ----------------------------------
 namespace rmr {
-hipError_t launch_trace(const KParams& P, int variant, bool persistent, int grid, hipStream_t s) {
+#define RMR_TRACE_SWITCH(V, NPV, PERS, PRG, CALL)        \
+    switch (NPV) {                                          \
+    case 4: CALL(V, 4, PERS, PRG); break;                   \
+    case 8: CALL(V, 8, PERS, PRG); break;                   \
+    case 0: CALL(V, 0, PERS, PRG); break;                   \
+    default: CALL(V, -1, PERS, PRG); break;                 \
+    }
+#define RMR_LAUNCH(V, NPV, PERS, PRG) k_trace<V, NPV, PERS, PRG><<<g, block, 0, s>>>(P)
+
+hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool persistent, int grid, hipStream_t s) {
     dim3 block(256);
+    unsigned g = (unsigned)grid;
     if (persistent) {
         switch (variant) {
-        case RMR_VARIANT_RM1: k_trace<RMR_VARIANT_RM1, true><<<grid, block, 0, s>>>(P); break;
-        case RMR_VARIANT_RM2: k_trace<RMR_VARIANT_RM2, true><<<grid, block, 0, s>>>(P); break;
-        default: k_trace<RMR_VARIANT_RM3, true><<<grid, block, 0, s>>>(P); break;
+        case RMR_VARIANT_RM1:
+            if (prog) { RMR_TRACE_SWITCH(RMR_VARIANT_RM1, np, true, true, RMR_LAUNCH); }
+            else { RMR_TRACE_SWITCH(RMR_VARIANT_RM1, np, true, false, RMR_LAUNCH); }
+            break;
+        case RMR_VARIANT_RM2: RMR_TRACE_SWITCH(RMR_VARIANT_RM2, np, true, false, RMR_LAUNCH); break;
+        default: RMR_TRACE_SWITCH(RMR_VARIANT_RM3, np, true, false, RMR_LAUNCH); break;
         }
     } else {
-        const uint64_t blocks = (P.n_units + 255) / 256;
+        g = (unsigned)((P.n_units + 255) / 256);
         switch (variant) {
-        case RMR_VARIANT_RM1: k_trace<RMR_VARIANT_RM1, false><<<(unsigned)blocks, block, 0, s>>>(P); break;
-        case RMR_VARIANT_RM2: k_trace<RMR_VARIANT_RM2, false><<<(unsigned)blocks, block, 0, s>>>(P); break;
-        default: k_trace<RMR_VARIANT_RM3, false><<<(unsigned)blocks, block, 0, s>>>(P); break;
+        case RMR_VARIANT_RM1: RMR_LAUNCH(RMR_VARIANT_RM1, -1, false, true); break;
+        case RMR_VARIANT_RM2: RMR_LAUNCH(RMR_VARIANT_RM2, -1, false, false); break;
+        default: RMR_LAUNCH(RMR_VARIANT_RM3, -1, false, false); break;
         }
     }
     return hipGetLastError();
@@ -860,13 +944,17 @@ hipError_t launch_fold(const KParams& P, hipStream_t s) {
     k_fold<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(P);
     return hipGetLastError();
 }
-int trace_occupancy(int variant, int* blocks_per_cu) {
+#define RMR_OCC(V, NPV, PERS, PRG) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace<V, NPV, PERS, PRG>, 256, 0)
+int trace_occupancy(int variant, int np, bool prog, int* blocks_per_cu) {
     int b = 0;
-    hipError_t e;
+    hipError_t e = hipSuccess;
     switch (variant) {
-    case RMR_VARIANT_RM1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace<RMR_VARIANT_RM1, true>, 256, 0); break;
-    case RMR_VARIANT_RM2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace<RMR_VARIANT_RM2, true>, 256, 0); break;
-    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace<RMR_VARIANT_RM3, true>, 256, 0); break;
+    case RMR_VARIANT_RM1:
+        if (prog) { RMR_TRACE_SWITCH(RMR_VARIANT_RM1, np, true, true, RMR_OCC); }
+        else { RMR_TRACE_SWITCH(RMR_VARIANT_RM1, np, true, false, RMR_OCC); }
+        break;
+    case RMR_VARIANT_RM2: RMR_TRACE_SWITCH(RMR_VARIANT_RM2, np, true, false, RMR_OCC); break;
+    default: RMR_TRACE_SWITCH(RMR_VARIANT_RM3, np, true, false, RMR_OCC); break;
     }
     *blocks_per_cu = b;
     return e == hipSuccess ? 0 : -1;
