@@ -91,20 +91,15 @@ def main():
         r.set_kernel(args.kernel)
     if args.shade_threshold:
         r.set_tuning(shade_threshold=args.shade_threshold)
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer
     stream = torch.cuda.current_stream()
     r.set_stream(stream.cuda_stream)
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-    r.bind_accum(acc.data_ptr(), acc.numel() * 4)
-
-    tiles = [(tx, ty) for ty in range((H + TILE - 1) // TILE) for tx in range((W + TILE - 1) // TILE)]
-    mine = np.array(tiles[rank::world], np.int32)
+    fr = FrameRenderer(r, acc, W, H, TILE, rank, world, dist if dist_on else None)
     times = time_schedule(args.spp)
 
     def step():
-        acc.zero_()
-        r.render_tiles(times, mine, TILE)
-        if dist_on:
-            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        fr.frame(times)
 
     for _ in range(args.warmup):
         step()

@@ -95,6 +95,12 @@ void rmr_camera_view(const double eye[3], const double dir[3], float aspect, flo
  * compile it into tables. Errors the reference would hit as a GLSL compile error (stale arity,
  * unknown node, bad var index) return RMR_E_SCENE with the message in rmr_last_error. */
 int rmr_load_scene_json(rmr_ctx* ctx, int variant, const char* json, size_t len);
+/* Context-free scene compilation (no GPU needed): compile to a library-owned table set, view it
+ * as an rmr_scene, free it. On RMR_E_SCENE the reason is written to err (if errlen > 0). */
+typedef struct rmr_scene_blob rmr_scene_blob;
+int rmr_scene_compile(int variant, const char* json, size_t len, rmr_scene_blob** out, char* err, size_t errlen);
+int rmr_scene_view(const rmr_scene_blob* blob, rmr_scene* out);
+void rmr_scene_free(rmr_scene_blob* blob);
 /* Load precompiled tables (copied). */
 int rmr_load_scene_tables(rmr_ctx* ctx, const rmr_scene* scene);
 /* The built-in scenes that the reference hard-codes in its shaders: RM2's one-sphere map

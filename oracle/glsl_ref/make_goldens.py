@@ -1,0 +1,142 @@
+"""oracle/glsl_ref/make_goldens.py — TEST INFRASTRUCTURE: generate tests/golden/ fixtures by running
+the reference GLSL (RayMarch*.glsl from /root/reference) on Mesa llvmpipe in this container.
+
+    python -m oracle.glsl_ref.make_goldens [--only NAME] [--conv-spp N]
+
+Fixtures are data (inputs + reference outputs); the reference source itself is not stored.
+  kat_<scene>.npz   function-level known answers: map / march / getNormal / rand chain /
+                    randHemisphere on fixed input sets (+ wavelengthToColor for RM3)
+  img_<name>.npz    low-spp renders (4 spp) and converged renders (--conv-spp) of 64x48 images
+MANIFEST.json records every configuration, the camera, the seed schedule and the GL driver.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from oracle import camera  # noqa: E402
+from oracle.glsl_ref import ref_run, shader_build  # noqa: E402
+from raymarchrenderer_amd import abi, time_schedule  # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+GS = os.path.join(GOLDEN, "scenes")
+W, H = 64, 48
+
+# name: (scene file or None, variant, params overrides, converged spp)
+IMAGES = {
+    "rm3_builtin": (None, 3, {}, 16384),
+    "rm1_cornell5_b4": (os.path.join(ROOT, "scenes", "cornell5.scene"), 1, {"max_bounces": 4}, 16384),
+    "rm1_sphere1_b1": (os.path.join(ROOT, "scenes", "sphere1.scene"), 1, {"max_bounces": 1}, 4096),
+    "rm2_simple": (os.path.join(GS, "simple.scene"), 2, {}, 16384),
+    "rm1_default": (os.path.join(GS, "default.scene"), 1, {}, 8192),
+    "rm1_glass": (os.path.join(GS, "glass_test.scene"), 1, {}, 8192),
+    "rm1_multilight": (os.path.join(GS, "multilight.scene"), 1, {}, 8192),
+}
+KATS = {
+    "rm3": (None, 3),
+    "cornell5": (os.path.join(ROOT, "scenes", "cornell5.scene"), 1),
+    "default": (os.path.join(GS, "default.scene"), 1),
+}
+
+
+def _scene(path):
+    return shader_build.load_scene(path) if path else None
+
+
+def make_kat(name, path, variant, rng):
+    scene = _scene(path)
+    prm = abi.default_params()
+    n = 512
+    pts = rng.uniform([-5, -1.5, -5], [5, 5, 5], size=(n, 3)).astype(np.float32)
+    m = ref_run.probe(variant, scene, 0, pts, n, 2, prm)
+    eye = np.array([0, 4, -6], np.float32)
+    o = (eye + rng.normal(0, 0.3, size=(n, 3))).astype(np.float32)
+    d = rng.normal(0, 1, size=(n, 3))
+    d[:, 1] = -np.abs(d[:, 1])
+    d[:, 2] = np.abs(d[:, 2])
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    march = ref_run.probe(variant, scene, 1, np.concatenate([o, d], 1), n, 2, prm)
+    # normals at march hit points
+    hits = (o + d * march[:, :1]).astype(np.float32)
+    nrm = ref_run.probe(variant, scene, 2, hits, n, 3, prm)
+    seeds = rng.uniform(-50, 1500, size=(n, 8)).astype(np.float32)
+    t = 0.512
+    rnd = ref_run.probe(variant, scene, 3, seeds, n, 4, prm, time=t)
+    hin = np.concatenate([rng.uniform(-5, 5, size=(n, 4)), rng.normal(0, 1, size=(n, 3)),
+                          np.zeros((n, 1)), rng.uniform(0, 1, size=(n, 1))], 1).astype(np.float32)
+    hin[:, 4:7] /= np.linalg.norm(hin[:, 4:7], axis=1, keepdims=True)
+    hemi = ref_run.probe(variant, scene, 4, hin, n, 3, prm, time=t)
+    out = dict(map_in=pts, map_out=m, march_in=np.concatenate([o, d], 1), march_out=march, normal_in=hits,
+               normal_out=nrm, rand_in=seeds, rand_out=rnd, rand_time=np.float32(t), hemi_in=hin, hemi_out=hemi,
+               probe_width=np.int32(64))
+    if variant == 3:
+        wls = np.arange(360, 860, dtype=np.float32)
+        out["wl_in"] = wls
+        out["wl_out"] = ref_run.wl2rgb_probe(wls)
+    np.savez_compressed(os.path.join(GOLDEN, "kat_%s.npz" % name), **out)
+
+
+def make_image(name, path, variant, kw, conv_spp, threads):
+    scene = _scene(path)
+    prm = abi.default_params(**kw)
+    view = camera.default_view(W, H)
+    lo = ref_run.render(variant, scene, W, H, time_schedule(4), prm, view, threads=threads)
+    t0 = time.time()
+    conv = ref_run.render(variant, scene, W, H, time_schedule(conv_spp), prm, view, threads=threads)
+    dt = time.time() - t0
+    np.savez_compressed(os.path.join(GOLDEN, "img_%s.npz" % name), lo=lo, conv=conv, view=view,
+                        spp_lo=np.int32(4), spp_conv=np.int32(conv_spp))
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--conv-scale", type=float, default=1.0)
+    args = ap.parse_args()
+    if not ref_run.available():
+        sys.exit("reference or Mesa swrast driver not available")
+    ref_run.ensure_built()
+    os.makedirs(GOLDEN, exist_ok=True)
+    man_path = os.path.join(GOLDEN, "MANIFEST.json")
+    man = json.load(open(man_path)) if os.path.exists(man_path) else {}
+    gl = subprocess.run(["bash", "-c", "RMR_VERBOSE=1 true"], capture_output=True, text=True)
+    _ = gl
+    man["generator"] = "oracle/glsl_ref/make_goldens.py (reference GLSL on Mesa llvmpipe via oracle/glsl_ref/harness.c)"
+    man["driver"] = "Mesa 23.2.1 llvmpipe (swrast_dri.so), GL 4.5 core"
+    man["image_size"] = [W, H]
+    man["camera"] = "Program.cpp:102 default camera, aspect W/H"
+    man["time_schedule"] = "time(f=0, s) = 0.016 * s, s = 0..spp-1 (float32)"
+    man.setdefault("kat", {})
+    man.setdefault("images", {})
+    rng = np.random.default_rng(20251015)
+    for name, (path, variant) in KATS.items():
+        if args.only and args.only != "kat_" + name:
+            continue
+        make_kat(name, path, variant, rng)
+        man["kat"][name] = {"scene": os.path.relpath(path, ROOT) if path else "builtin", "variant": variant}
+        print("kat", name, flush=True)
+    for name, (path, variant, kw, spp) in IMAGES.items():
+        if args.only and args.only != name:
+            continue
+        spp = int(spp * args.conv_scale)
+        dt = make_image(name, path, variant, kw, spp, args.threads)
+        man["images"][name] = {"scene": os.path.relpath(path, ROOT) if path else "builtin", "variant": variant,
+                               "params": kw, "spp_lo": 4, "spp_conv": spp, "seconds": round(dt, 1)}
+        print("image", name, spp, "spp", round(dt, 1), "s", flush=True)
+        with open(man_path, "w") as f:
+            json.dump(man, f, indent=1, sort_keys=True)
+    with open(man_path, "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

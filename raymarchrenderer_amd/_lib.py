@@ -21,6 +21,7 @@ EXPORTS = [
     "rmr_accum_device_ptr", "rmr_bind_accum", "rmr_save_bmp", "rmr_encode_bmp",
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats",
     "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes",
+    "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free",
 ]
 
 
@@ -80,6 +81,9 @@ def lib():
         "rmr_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_longlong]),
         "rmr_trace_samples": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, fp]),
         "rmr_abi_sizes": (C.c_int, [C.POINTER(C.c_int32), C.c_int]),
+        "rmr_scene_compile": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
+        "rmr_scene_view": (C.c_int, [vp, C.POINTER(abi.Scene)]),
+        "rmr_scene_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

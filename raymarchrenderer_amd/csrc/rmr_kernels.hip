@@ -193,19 +193,42 @@ RMR_D void opu(V2& d, float dj, float mid) {
     d.y = keep ? d.y : mid;
 }
 
-template <int NP>
-RMR_D V2 map_fixed(const KParams& P, V3 p) {
-    CDPrim* pr = (CDPrim*)P.dprims;
+// sphere / box with the short correctly-rounded sqrt (valid unless `tiny` is raised)
+RMR_D float sd_sphere_f(V3 p, V3 c, float r, bool& tiny) { return length_fast(p - c, tiny) - r; }
+RMR_D float sd_box_f(V3 p, V3 c, V3 r, bool& tiny) {
+    V3 q = vabs(p - c) - r;
+    return fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f) + length_fast(vmax0(q), tiny);
+}
+
+// one scalar load per prim: the 32-byte DPrim as a single s_load_dwordx8
+typedef int int8v __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) int8v CInt8v;
+
+template <int NP, bool EXACT>
+RMR_D V2 map_fixed_impl(const KParams& P, V3 p, bool& tiny) {
+    CInt8v* pr = (CInt8v*)P.dprims;
     V2 d = v2(P.max_dist, -1.0f);
+    int8v cur = pr[0];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const int type = pr[j].type;
-        const V3 c = v3(pr[j].c[0], pr[j].c[1], pr[j].c[2]);
-        const V3 r = v3(pr[j].r[0], pr[j].r[1], pr[j].r[2]);
-        const float mid = pr[j].mat_id;
-        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
-        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
+        int8v nxt;
+        if (j + 1 < NP) nxt = pr[j + 1];   // next prim in flight while this one is evaluated
+        const int type = cur[6];
+        const V3 c = v3(__int_as_float(cur[0]), __int_as_float(cur[1]), __int_as_float(cur[2]));
+        const V3 r = v3(__int_as_float(cur[3]), __int_as_float(cur[4]), __int_as_float(cur[5]));
+        const float mid = __int_as_float(cur[7]);
+        if (type == RMR_PRIM_BOX) opu(d, EXACT ? sd_box(p, c, r) : sd_box_f(p, c, r, tiny), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, EXACT ? sd_sphere(p, c, r.x) : sd_sphere_f(p, c, r.x, tiny), mid);
+        if (j + 1 < NP) cur = nxt;
     }
+    return d;
+}
+
+template <int NP>
+RMR_D V2 map_fixed(const KParams& P, V3 p) {
+    bool tiny = false;
+    V2 d = map_fixed_impl<NP, false>(P, p, tiny);
+    if (tiny) d = map_fixed_impl<NP, true>(P, p, tiny);   // some sqrt input in (0, 2^-96): redo exactly
     return d;
 }
 

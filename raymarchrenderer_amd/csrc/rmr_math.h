@@ -204,3 +204,22 @@ RMR_D float det_atan2(float y, float x) {
 }
 
 }  // namespace rmr
+
+namespace rmr {
+// Correctly rounded sqrt for x == 0 or x >= 2^-96 (and NaN): v_sqrt_f32 (<= 1 ulp) + the one-ulp
+// fix-up of hipcc's IEEE lowering, without its tiny-input rescaling. `tiny` is raised for
+// 0 < x < 2^-96, where the caller must redo the computation with sqrtf(). Verified exhaustively
+// against sqrtf on gfx950 (tools/probes/sqrt_exhaustive.hip).
+RMR_D float sqrt_cr_fast(float x, bool& tiny) {
+    tiny = tiny || (x < 0x1p-96f && x > 0.0f);
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = fmaf(-sm, s, x);
+    const float rp = fmaf(-sp, s, x);
+    s = (rm <= 0.0f) ? sm : s;
+    s = (rp > 0.0f) ? sp : s;
+    return s;
+}
+RMR_D float length_fast(V3 a, bool& tiny) { return sqrt_cr_fast(dot(a, a), tiny); }
+}  // namespace rmr

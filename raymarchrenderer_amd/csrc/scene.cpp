@@ -470,3 +470,34 @@ CompiledScene builtin_scene(int variant) {
 }
 
 }  // namespace rmr
+
+// ---- context-free C ABI ----------------------------------------------------------------------
+struct rmr_scene_blob {
+    rmr::CompiledScene sc;
+};
+
+extern "C" int rmr_scene_compile(int variant, const char* json, size_t len, rmr_scene_blob** out, char* err,
+                                 size_t errlen) {
+    if (!json || !out) return -1;
+    *out = nullptr;
+    try {
+        rmr_scene_blob* b = new rmr_scene_blob();
+        if (variant == RMR_VARIANT_RM3 && len == 0) b->sc = rmr::builtin_scene(variant);
+        else b->sc = rmr::compile_scene(std::string(json, len), variant);
+        *out = b;
+        return 0;
+    } catch (const std::exception& e) {
+        if (err && errlen) {
+            std::snprintf(err, errlen, "%s", e.what());
+        }
+        return -3;
+    }
+}
+
+extern "C" int rmr_scene_view(const rmr_scene_blob* b, rmr_scene* out) {
+    if (!b || !out) return -1;
+    *out = b->sc.view();
+    return 0;
+}
+
+extern "C" void rmr_scene_free(rmr_scene_blob* b) { delete b; }

@@ -1,0 +1,61 @@
+"""Converged-radiance parity with the reference GLSL (BASELINE north star: PSNR >= 40 dB).
+
+The reference images are llvmpipe renders of RayMarch*.glsl at 16k-64k spp (tests/golden/img_*.npz,
+seed schedule time = 0.016 s). The GPU renders 4x as many samples over the same time range
+(time = 0.004 k): the reference hash's quality depends on the magnitude of `time`, so equal ranges
+give equally distributed (but independent) sample streams. PSNR is over linear RGB clamped to
+[0, 1]; the floor is set by the reference's own Monte-Carlo noise (printed with each result).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from raymarchrenderer_amd import abi
+
+from .conftest import GOLDEN, SCENES
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # name: (scene, variant, params, min PSNR dB)
+    "rm3_builtin": (None, "rm3", {}, 40.0),
+    "rm1_cornell5_b4": (os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 4}, 40.0),
+    "rm1_sphere1_b1": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 1}, 40.0),
+    "rm2_simple": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {}, 40.0),
+    "rm1_glass": (os.path.join(GOLDEN, "scenes", "glass_test.scene"), "rm1", {}, 35.0),
+    "rm1_multilight": (os.path.join(GOLDEN, "scenes", "multilight.scene"), "rm1", {}, 35.0),
+    "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}, 35.0),
+}
+
+
+def psnr(a, b):
+    a = np.clip(a[..., :3].astype(np.float64), 0, 1)
+    b = np.clip(b[..., :3].astype(np.float64), 0, 1)
+    return 10 * np.log10(1.0 / max(np.mean((a - b) ** 2), 1e-30))
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_converged_psnr_vs_reference(renderer, name):
+    path, variant, kw, floor = CASES[name]
+    g = np.load(os.path.join(GOLDEN, "img_%s.npz" % name))
+    ref = g["conv"]
+    H, W = ref.shape[:2]
+    n_ref = int(g["spp_conv"])
+    renderer.set_image_size(W, H)
+    renderer.reload()
+    if path is None:
+        renderer.load_builtin(variant)
+    else:
+        renderer.load_scene(path, variant)
+    renderer.set_params(abi.default_params(**kw))
+    renderer.set_view(g["view"])
+    n = 4 * n_ref
+    times = (np.arange(n, dtype=np.float64) * (0.016 / 4)).astype(np.float32)
+    renderer.render_spp(times)
+    img = renderer.read_accum()
+    p = psnr(img, ref)
+    rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(ref[..., :3].mean(), 1e-12)
+    print("%s: PSNR %.2f dB vs reference @%d spp (GPU %d spp), mean rel diff %+.4f" % (name, p, n_ref, n, rel))
+    assert p >= floor
+    assert abs(rel) < 0.02

@@ -1,0 +1,74 @@
+"""Multi-rank path on CPU (gloo, world size 2): the tile partition + one reduce reproduce the
+single-process frame bit for bit. The per-rank renderer here is the CPU oracle (test
+infrastructure); on the GPU box bench.py runs the same partition through librmr over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import camera, oracle, scene_compile
+from raymarchrenderer_amd import abi, time_schedule
+from raymarchrenderer_amd.multi_gpu import frame_tiles, reduce_frame, tile_partition
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W, H, TILE = 40, 24, 16
+
+
+def _render_tiles(tiles, times):
+    t = scene_compile.load_scene_file(os.path.join(ROOT, "scenes", "cornell5.scene"), "rm1")
+    o = oracle.Oracle(t, abi.default_params(max_bounces=3), camera.default_view(W, H), W, H)
+    acc = np.zeros((H, W, 4), np.float32)
+    for tx, ty in tiles:
+        o.render(times, rect=(tx * TILE, ty * TILE, min(W, (tx + 1) * TILE), min(H, (ty + 1) * TILE)),
+                 accum=acc, nthreads=2)
+    return acc
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    times = time_schedule(2)
+    acc = torch.from_numpy(_render_tiles(tile_partition(W, H, TILE, rank, world), times))
+    reduce_frame(acc, dist)
+    if rank == 0:
+        q.put(acc.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_partition_covers_frame_once():
+    for world in (1, 2, 3, 8):
+        parts = [set(map(tuple, tile_partition(1920, 1080, 32, r, world))) for r in range(world)]
+        assert sum(len(p) for p in parts) == len(frame_tiles(1920, 1080, 32))
+        assert set().union(*parts) == set(frame_tiles(1920, 1080, 32))
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_ranks_reduce_is_exact():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _render_tiles(frame_tiles(W, H, TILE), time_schedule(2))
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
