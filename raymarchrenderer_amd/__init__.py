@@ -7,7 +7,7 @@ reference's Graphics / Camera / Screen host interfaces.
 from . import abi
 from ._lib import RMRError, lib
 from .renderer import (Camera, Graphics, Renderer, Screen, camera_view, default_camera_view, encode_bmp,
-                       save_name, tile_spiral, time_schedule)
+                       parity_schedule, save_name, tile_spiral, time_schedule)
 
 __all__ = ["abi", "lib", "RMRError", "Renderer", "Graphics", "Camera", "Screen", "camera_view",
-           "default_camera_view", "encode_bmp", "tile_spiral", "time_schedule", "save_name"]
+           "default_camera_view", "encode_bmp", "tile_spiral", "time_schedule", "parity_schedule", "save_name"]

@@ -193,42 +193,29 @@ RMR_D void opu(V2& d, float dj, float mid) {
     d.y = keep ? d.y : mid;
 }
 
-// sphere / box with the short correctly-rounded sqrt (valid unless `tiny` is raised)
-RMR_D float sd_sphere_f(V3 p, V3 c, float r, bool& tiny) { return length_fast(p - c, tiny) - r; }
-RMR_D float sd_box_f(V3 p, V3 c, V3 r, bool& tiny) {
-    V3 q = vabs(p - c) - r;
-    return fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f) + length_fast(vmax0(q), tiny);
-}
-
-// one scalar load per prim: the 32-byte DPrim as a single s_load_dwordx8
+// One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
+// in flight while prim j is evaluated (A/B: +2% over loading at use). The IEEE sqrt sequence hipcc
+// emits was measured FASTER here than rmr::sqrt_cr_fast + a tiny-input fallback (17.0 vs 18.4 ms).
 typedef int int8v __attribute__((ext_vector_type(8)));
 typedef const __attribute__((address_space(4))) int8v CInt8v;
 
-template <int NP, bool EXACT>
-RMR_D V2 map_fixed_impl(const KParams& P, V3 p, bool& tiny) {
+template <int NP>
+RMR_D V2 map_fixed(const KParams& P, V3 p) {
     CInt8v* pr = (CInt8v*)P.dprims;
     V2 d = v2(P.max_dist, -1.0f);
     int8v cur = pr[0];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         int8v nxt;
-        if (j + 1 < NP) nxt = pr[j + 1];   // next prim in flight while this one is evaluated
+        if (j + 1 < NP) nxt = pr[j + 1];
         const int type = cur[6];
         const V3 c = v3(__int_as_float(cur[0]), __int_as_float(cur[1]), __int_as_float(cur[2]));
         const V3 r = v3(__int_as_float(cur[3]), __int_as_float(cur[4]), __int_as_float(cur[5]));
         const float mid = __int_as_float(cur[7]);
-        if (type == RMR_PRIM_BOX) opu(d, EXACT ? sd_box(p, c, r) : sd_box_f(p, c, r, tiny), mid);
-        else if (type == RMR_PRIM_SPHERE) opu(d, EXACT ? sd_sphere(p, c, r.x) : sd_sphere_f(p, c, r.x, tiny), mid);
+        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
         if (j + 1 < NP) cur = nxt;
     }
-    return d;
-}
-
-template <int NP>
-RMR_D V2 map_fixed(const KParams& P, V3 p) {
-    bool tiny = false;
-    V2 d = map_fixed_impl<NP, false>(P, p, tiny);
-    if (tiny) d = map_fixed_impl<NP, true>(P, p, tiny);   // some sqrt input in (0, 2^-96): redo exactly
     return d;
 }
 
@@ -442,28 +429,25 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
     }
 }
 
-// getNormal probe order: +x, -x, +y, -y, +z, -z (RM1:263-265)
+// getNormal probe order: +x, -x, +y, -y, +z, -z (RM1:263-265).
+// +probes add (+h, +0, +0); -probes add (-h, -0, -0): x + (-0) == x - 0 bit for bit, so this is
+// exactly the oracle's p +- vec3(h,0,0) without a divergent switch (A/B: +10% vs a switch).
 RMR_D V3 probe_point(const Lane& L) {
     const float h = 0.001f;
-    const V3 p = L.hit;
-    switch (L.probe) {
-    case 0: return v3(p.x + h, p.y + 0.0f, p.z + 0.0f);
-    case 1: return v3(p.x - h, p.y - 0.0f, p.z - 0.0f);
-    case 2: return v3(p.x + 0.0f, p.y + h, p.z + 0.0f);
-    case 3: return v3(p.x - 0.0f, p.y - h, p.z - 0.0f);
-    case 4: return v3(p.x + 0.0f, p.y + 0.0f, p.z + h);
-    default: return v3(p.x - 0.0f, p.y - 0.0f, p.z - h);
-    }
+    const int ax = L.probe >> 1;
+    const bool neg = (L.probe & 1) != 0;
+    const float hs = neg ? -h : h, z0 = neg ? -0.0f : 0.0f;
+    return v3(L.hit.x + (ax == 0 ? hs : z0), L.hit.y + (ax == 1 ? hs : z0), L.hit.z + (ax == 2 ? hs : z0));
 }
 RMR_D void normal_update(Lane& L, float m) {
-    switch (L.probe) {
-    case 0: L.nplus.x = m; break;
-    case 1: L.nrm.x = L.nplus.x - m; break;
-    case 2: L.nplus.y = m; break;
-    case 3: L.nrm.y = L.nplus.y - m; break;
-    case 4: L.nplus.z = m; break;
-    default: L.nrm.z = L.nplus.z - m; break;
-    }
+    const int ax = L.probe >> 1;
+    const bool plus = (L.probe & 1) == 0;
+    L.nplus.x = (plus && ax == 0) ? m : L.nplus.x;
+    L.nplus.y = (plus && ax == 1) ? m : L.nplus.y;
+    L.nplus.z = (plus && ax == 2) ? m : L.nplus.z;
+    L.nrm.x = (!plus && ax == 0) ? L.nplus.x - m : L.nrm.x;
+    L.nrm.y = (!plus && ax == 1) ? L.nplus.y - m : L.nrm.y;
+    L.nrm.z = (!plus && ax == 2) ? L.nplus.z - m : L.nrm.z;
     L.probe++;
     if (L.probe == 6) {
         L.nrm = normalize(L.nrm);
@@ -820,8 +804,11 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 // ------------------------------------------------------------------------------------------
 // the trace kernel
 // ------------------------------------------------------------------------------------------
+// Occupancy target (waves per SIMD) for the fast specialisations: the kernel is latency-bound
+// (scalar-load and dependent-chain stalls), and 8 waves/SIMD measured +8% over the 5 that the
+// register allocator picks unconstrained. The general/interpreter kernels keep their registers.
 template <int VAR, int NP, bool PERSIST, bool PROG>
-__global__ __launch_bounds__(256) void k_trace(KParams P) {
+__global__ __launch_bounds__(256, ((NP < 0 || PROG || VAR == RMR_VARIANT_RM2) ? 1 : 8)) void k_trace(KParams P) {
     Lane L;
     L.phase = PH_IDLE;
     uint64_t maps = 0, iters = 0, shades = 0;

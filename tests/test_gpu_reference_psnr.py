@@ -1,17 +1,19 @@
 """Converged-radiance parity with the reference GLSL (BASELINE north star: PSNR >= 40 dB).
 
-The reference images are llvmpipe renders of RayMarch*.glsl at 16k-64k spp (tests/golden/img_*.npz,
-seed schedule time = 0.016 s). The GPU renders 4x as many samples over the same time range
-(time = 0.004 k): the reference hash's quality depends on the magnitude of `time`, so equal ranges
-give equally distributed (but independent) sample streams. PSNR is over linear RGB clamped to
-[0, 1]; the floor is set by the reference's own Monte-Carlo noise (printed with each result).
+The reference images are llvmpipe renders of RayMarch*.glsl at 16k-256k spp (tests/golden/img_*.npz)
+on raymarchrenderer_amd.parity_schedule (time = s * 0.016/256). The GPU renders the SAME schedule:
+the reference's chained sin-hash is not a uniform RNG — its distribution depends on the seed
+values, and for large seeds on the driver's float32 sin() rounding (at time ~ 4000 two
+implementations' Cornell-5 means differ by 8.7%), so a converged image is only comparable on a
+shared, small-seed schedule. The two streams are still independent (the hash is chaotic), so PSNR is
+bounded by both sides' Monte-Carlo noise. PSNR is over linear RGB clamped to [0, 1].
 """
 import os
 
 import numpy as np
 import pytest
 
-from raymarchrenderer_amd import abi
+from raymarchrenderer_amd import abi, parity_schedule
 
 from .conftest import GOLDEN, SCENES
 
@@ -50,9 +52,8 @@ def test_converged_psnr_vs_reference(renderer, name):
         renderer.load_scene(path, variant)
     renderer.set_params(abi.default_params(**kw))
     renderer.set_view(g["view"])
-    n = 4 * n_ref
-    times = (np.arange(n, dtype=np.float64) * (0.016 / 4)).astype(np.float32)
-    renderer.render_spp(times)
+    n = n_ref
+    renderer.render_spp(parity_schedule(n))
     img = renderer.read_accum()
     p = psnr(img, ref)
     rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(ref[..., :3].mean(), 1e-12)
