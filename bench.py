@@ -1,10 +1,17 @@
 """bench.py — headline benchmark: Msamples/s (pixels x spp) of the SDF ray-march path tracer.
 
-Workload (BASELINE.json configs[1]): Cornell-5 SDF scene (scenes/cornell5.scene,
-RayMarch.glsl semantics), 1920x1080, 64 spp, 4 bounces, default camera (Program.cpp:102), seed
-schedule time(f, s) = 1000 f + 0.016 s. One step = one full frame at 64 spp: every pixel's 64
-samples traced, folded into the RGBA32F running mean, and (N > 1) the per-rank tile accumulators
-summed onto rank 0 by one RCCL reduce.
+Default workload (BASELINE.json configs[1]): Cornell-5 SDF scene
+(scenes/cornell5.scene, RayMarch.glsl semantics), 1920x1080, 64 spp, 4 bounces, default camera
+(Program.cpp:102), seed schedule time(f, s) = 1000 f + 0.016 s. One step = one full frame: every
+pixel's spp samples traced, folded into the RGBA32F running mean, and (N > 1) the per-rank tile
+accumulators summed onto rank 0 by one RCCL reduce.
+
+The other BASELINE configs run with --config (they are separate bench lines, not the headline):
+  c1  single sphere 256x256, 1 spp, 1 bounce
+  c3  Mandelbulb (scenes/mandelbulb.scene) 1920x1080, 128 spp, 2 bounces
+  c4  256-prim union (scenes/csg256.scene) 3840x2160, 256 spp, 4 bounces
+  c5  animated Cornell-5, 1920x1080, 512 spp, 4 bounces: step f renders frame f (sphere centre
+      y = 0.5 sin(2 pi f / 120)); the scene is recompiled and uploaded inside the timed step
 
 Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL). The frame's 32x32 tiles
 are dealt round-robin to the ranks; each rank renders its tiles into a zeroed full-frame
@@ -14,20 +21,26 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/sec (pixels×spp) at 1920×1080; PSNR vs GLSL reference"
-W, H, SPP, BOUNCES = 1920, 1080, 64, 4
 TILE = 32
-SCENE = os.path.join(ROOT, "scenes", "cornell5.scene")
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
+
+CONFIGS = {
+    "c1": dict(scene="sphere1.scene", W=256, H=256, spp=1, bounces=1, name="C1 single-sphere SDF"),
+    "c2": dict(scene="cornell5.scene", W=1920, H=1080, spp=64, bounces=4, name="C2 Cornell-5 SDF"),
+    "c3": dict(scene="mandelbulb.scene", W=1920, H=1080, spp=128, bounces=2, name="C3 Mandelbulb SDF"),
+    "c4": dict(scene="csg256.scene", W=3840, H=2160, spp=256, bounces=4, name="C4 256-prim CSG union"),
+    "c5": dict(scene="cornell5.scene", W=1920, H=1080, spp=512, bounces=4, name="C5 animated Cornell-5",
+               animated=True),
+}
 
 
 def parse():
@@ -35,24 +48,39 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=SPP)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel", type=int, default=0, help="0 persistent, 1 per-path")
     ap.add_argument("--shade-threshold", type=int, default=0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
+    ap.add_argument("--traffic-json", default="")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds, spp, threads):
-    """CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload: every
-    27th image row (40 rows x 1920 px) of the C2 frame, samples 0.. of the same schedule,
-    repeated until ~`seconds` of CPU time."""
+def scene_for_frame(cfg, frame):
+    """Scene dict for a frame: static configs return the file; C5 moves the Cornell sphere
+    (objects[3]) to y = 0.5 sin(2 pi f / 120)."""
+    path = os.path.join(ROOT, "scenes", cfg["scene"])
+    if not cfg.get("animated"):
+        return path
+    with open(path) as f:
+        sc = json.load(f)
+    sc["objects"][3]["nodes"][0]["inputs"][1][1] = 0.5 * math.sin(2.0 * math.pi * frame / 120.0)
+    return sc
+
+
+def cpu_baseline(cfg, spp, seconds, threads):
+    """CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload: 40 rows
+    spread over the frame, samples 0.. of the same schedule, repeated until ~`seconds` pass."""
     from oracle import camera, oracle, scene_compile
     from raymarchrenderer_amd import abi, time_schedule
-    t = scene_compile.load_scene_file(SCENE, "rm1")
-    o = oracle.Oracle(t, abi.default_params(max_bounces=BOUNCES), camera.default_view(W, H), W, H)
-    rows = list(range(0, H, 27))
+    W, H = cfg["W"], cfg["H"]
+    sc = scene_for_frame(cfg, 0)
+    t = scene_compile.load_scene_file(sc, "rm1") if isinstance(sc, str) else scene_compile.compile_scene(sc, "rm1")
+    o = oracle.Oracle(t, abi.default_params(max_bounces=cfg["bounces"]), camera.default_view(W, H), W, H)
+    stride = max(1, H // 40)
+    rows = list(range(0, H, stride))
     times = time_schedule(spp)
     done = 0
     t0 = time.perf_counter()
@@ -67,12 +95,15 @@ def cpu_baseline(seconds, spp, threads):
             break
     dt = time.perf_counter() - t0
     return {"value": done / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d samples: rows y%%27==0 of the C2 1920x1080 frame, 1 spp per row pass, "
-                      "%d-thread OpenMP C restatement (oracle/rmr_oracle.c)" % (done, threads)}
+            "sample": "%d samples: rows y%%%d==0 of the %dx%d frame, 1 spp per row pass, %d-thread OpenMP C "
+                      "restatement (oracle/rmr_oracle.c)" % (done, stride, W, H, threads)}
 
 
 def main():
     args = parse()
+    cfg = CONFIGS[args.config]
+    W, H, BOUNCES = cfg["W"], cfg["H"], cfg["bounces"]
+    spp = args.spp or cfg["spp"]
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -85,7 +116,7 @@ def main():
     from raymarchrenderer_amd import Renderer, abi, time_schedule
 
     r = Renderer(local_rank, W, H)
-    r.load_scene(SCENE, "rm1")
+    r.load_scene(scene_for_frame(cfg, 0), "rm1")
     r.set_params(abi.default_params(max_bounces=BOUNCES))
     if args.kernel:
         r.set_kernel(args.kernel)
@@ -96,10 +127,18 @@ def main():
     r.set_stream(stream.cuda_stream)
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     fr = FrameRenderer(r, acc, W, H, TILE, rank, world, dist if dist_on else None)
-    times = time_schedule(args.spp)
+    animated = bool(cfg.get("animated"))
+    static_times = time_schedule(spp)
+    frame_no = [0]
 
     def step():
-        fr.frame(times)
+        f = frame_no[0]
+        frame_no[0] += 1
+        if animated:
+            r.load_scene(scene_for_frame(cfg, f % 120), "rm1")
+            fr.frame(time_schedule(spp, frame=f % 120))
+        else:
+            fr.frame(static_times)
 
     for _ in range(args.warmup):
         step()
@@ -120,26 +159,22 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        # dominant-kernel numbers of rank 0 are reported; map evals summed for the roofline
-        me = torch.tensor([st.map_evals, st.trace_launches], dtype=torch.float64, device="cuda")
-        dist.all_reduce(me, op=dist.ReduceOp.SUM)
-        total_maps = float(me[0].item())
-    else:
-        total_maps = float(st.map_evals)
 
-    samples = float(W) * H * args.spp * args.steps
+    samples = float(W) * H * spp * args.steps
     value = samples / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
     roof = None
     if st.trace_launches > 0 and st.trace_ms > 0:
+        # rank 0's dominant kernel: its own map evals over its own launches
         per_launch_ms = st.trace_ms / st.trace_launches
         flops_per_launch = float(st.map_evals) / st.trace_launches * st.flops_per_map
         achieved = flops_per_launch / (per_launch_ms * 1e-3) / 1e12
         traffic = None
-        if os.path.exists(args.traffic_json):
+        tj = args.traffic_json or os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+        if os.path.exists(tj) and world == 1 and spp == cfg["spp"]:
             try:
-                with open(args.traffic_json) as f:
+                with open(tj) as f:
                     traffic = json.load(f).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -148,23 +183,23 @@ def main():
                 "kernel": "k_trace<RM1,persistent>", "avg_launch_ms": round(per_launch_ms, 3),
                 "map_evals_per_launch": int(st.map_evals / st.trace_launches),
                 "flops_per_map": st.flops_per_map,
-                "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1)}
+                "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
+                "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(args.cpu_seconds, args.spp, threads)
+        cpu = cpu_baseline(cfg, spp, args.cpu_seconds, threads)
 
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic",
-               "config": {"workload": "C2 Cornell-5 SDF (RayMarch.glsl semantics) 1920x1080 %d spp %d bounces"
-                                      % (args.spp, BOUNCES),
-                          "width": W, "height": H, "spp": args.spp, "max_bounces": BOUNCES,
-                          "samples_per_step": W * H * args.spp, "tile": TILE,
-                          "parallelism": "tiles%d" % world},
+               "config": {"workload": "%s (RayMarch.glsl semantics) %dx%d %d spp %d bounces"
+                                      % (cfg["name"], W, H, spp, BOUNCES),
+                          "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
+                          "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     r.close()

@@ -83,6 +83,50 @@ def make_kat(name, path, variant, rng):
     np.savez_compressed(os.path.join(GOLDEN, "kat_%s.npz" % name), **out)
 
 
+NAN_MAIN = r"""
+layout(std430, binding = 2) readonly buffer ProbeIn { float pin[]; };
+layout(std430, binding = 3) writeonly buffer ProbeOut { float pout[]; };
+uniform int probeCount;
+void main()
+{
+    uint gw = gl_NumWorkGroups.x * gl_WorkGroupSize.x;
+    uint i = gl_GlobalInvocationID.y * gw + gl_GlobalInvocationID.x;
+    if (i >= uint(probeCount)) return;
+    channels = vec3(1, 1, 1);
+    vec3 nanv = normalize(vec3(pin[4 * i + 3]));      // pin = 0: normalize(vec3(0)) = NaN
+    vec3 o = vec3(pin[4 * i], pin[4 * i + 1], pin[4 * i + 2]);
+    vec2 m = map(nanv);
+    vec2 a = march(o, nanv, 1.0);
+    vec2 b = march(o, nanv, -1.0);
+    pout[6 * i] = m.x; pout[6 * i + 1] = m.y;
+    pout[6 * i + 2] = a.x; pout[6 * i + 3] = a.y;
+    pout[6 * i + 4] = b.x; pout[6 * i + 5] = b.y;
+}
+"""
+
+
+def make_kat_nan(rng):
+    """NaN ray directions (normalize(vec3(0)) after total internal reflection in shader_refraction):
+    map(NaN) and march(o, NaN, +-1) of the reference on llvmpipe, per scene."""
+    import math
+    out = {}
+    for name, (path, variant) in KATS.items():
+        if variant != 1:
+            continue
+        n = 64
+        o = rng.uniform([-5, -1, -5], [5, 5, 5], size=(n, 3)).astype(np.float32)
+        pin = np.concatenate([o, np.zeros((n, 1), np.float32)], 1)
+        src = shader_build.build(variant, _scene(path), probe_main=NAN_MAIN)
+        lx, ly = shader_build.LOCAL[variant]
+        prm = abi.default_params()
+        lines = ["image 8 8"] + ref_run._uniform_lines(prm, np.zeros(15, np.float32))
+        lines += ["ui probeCount %d" % n, "run 0 0 0 0 0 0 %d %d" % (64 // lx, int(math.ceil(n / 64.0 / ly)))]
+        _, so = ref_run.run_job(src, lines, None, ssbo_in=pin.ravel(), ssbo_out_n=6 * n)
+        out["%s_origin" % name] = o
+        out["%s_out" % name] = so.reshape(n, 6)
+    np.savez_compressed(os.path.join(GOLDEN, "kat_nan.npz"), **out)
+
+
 def make_image(name, path, variant, kw, conv_spp, threads):
     scene = _scene(path)
     prm = abi.default_params(**kw)
@@ -126,6 +170,10 @@ def main():
         make_kat(name, path, variant, rng)
         man["kat"][name] = {"scene": os.path.relpath(path, ROOT) if path else "builtin", "variant": variant}
         print("kat", name, flush=True)
+    if not args.only or args.only == "kat_nan":
+        make_kat_nan(np.random.default_rng(7))
+        man["kat"]["nan"] = {"scenes": [k for k, v in KATS.items() if v[1] == 1], "probe": "map/march with NaN dir"}
+        print("kat nan", flush=True)
     for name, (path, variant, kw, spp) in IMAGES.items():
         if args.only and args.only != name:
             continue

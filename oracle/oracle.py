@@ -38,6 +38,7 @@ def lib():
         L.oracle_det_atan2.restype = C.c_float
         L.oracle_map.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
         L.oracle_march.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Params), fp, fp, C.c_float, fp]
+        L.oracle_trace.argtypes = [C.POINTER(Job), C.c_int, C.c_int, C.c_float, fp, fp, fp]
         L.oracle_normal.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
         L.oracle_rand_chain.argtypes = [C.c_int, C.c_int, C.c_float, fp, C.c_int, fp]
         L.oracle_hemisphere.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, fp, fp, fp, fp]
@@ -86,6 +87,13 @@ class Oracle:
                             _fp(accum), nthreads, C.byref(n))
         self.map_evals += n.value
         return accum
+
+    def trace(self, gx, gy, time, o, d):
+        """trace(o, d) of the reference for invocation (gx, gy), seed `time`, channels = 1."""
+        out = np.zeros(3, np.float32)
+        lib().oracle_trace(C.byref(self.job), gx, gy, C.c_float(time), _fp(np.asarray(o, np.float32)),
+                           _fp(np.asarray(d, np.float32)), _fp(out))
+        return out
 
     def trace_samples(self, times, rect=None, nthreads=0):
         times = np.ascontiguousarray(times, np.float32)

@@ -48,6 +48,9 @@ float oracle_det_acos(float x);
 float oracle_det_log(float x);
 float oracle_det_exp(float x);
 float oracle_det_atan2(float y, float x);
+/* trace(o, d) (RM1/RM2) for the invocation at gid (gx, gy), seed `time`, channels = 1 */
+void oracle_trace(const oracle_job* job, int gx, int gy, float time, const float o[3], const float d[3],
+                  float out[3]);
 /* map(p) -> (dist, id) */
 void oracle_map(const rmr_scene* sc, float max_dist, const float p[3], float out[2]);
 /* march(o,d,distMult) -> (t, id) */

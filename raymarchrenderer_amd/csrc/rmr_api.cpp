@@ -269,6 +269,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     const size_t plane = tiles.size() * 64;
     size_t chunk = std::max<size_t>(1, c->samp_budget / (plane * sizeof(float4)));
     chunk = std::min<size_t>(chunk, nspp);
+    // the trace kernel indexes units with 32 bits (atomic work counter included): < 2^31 per launch
+    chunk = std::max<size_t>(1, std::min<size_t>(chunk, ((size_t)1 << 31) / plane));
     if ((r = ensure_samp(c, plane * chunk))) return r;
     if (nspp > c->times_cap) {
         if (c->d_times) (void)hipFree(c->d_times);

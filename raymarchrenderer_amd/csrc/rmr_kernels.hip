@@ -41,40 +41,57 @@ enum Phase : int {
     PH_HIT = 4,     // march hit, normal ready: run the material
     PH_MISS = 5,    // march miss: sky
     PH_NEE = 6,     // RM2: shadow march finished
+    PH_RESTART = 7, // separateChannels: next channel's trace starts at the next refill point
 };
 
+// Per-lane path state. Kept small on purpose (the fast kernels run 8 waves/SIMD = 64 VGPRs):
+//  * the march sign (distMult, RM1:498-505) is `inside`; the march step counter and the
+//    getNormal probe index share `ctr`; getNormal accumulates +probe then subtracts -probe in nrm;
+//  * the primary direction is recomputed from `unit` when separateChannels restarts a trace;
+//  * the sample result goes straight to the sample plane (partial channel sums included);
+//  * HO kernels (hit-in-origin: RM1 without node programs, RM3) keep the hit point in `o`: the
+//    ray origin is dead between a hit and the next bounce there. RM2 (shadow ray from the hit) and
+//    node-program materials (ray.origin is an input of shader_mix / volumeScatter) keep `hit`.
 struct Lane {
-    uint64_t unit;
-    int px, py;
-    float time, gxt, gyt, rc;
+    uint32_t unit;
+    float gxt, gyt, rc;
     V3 o, d;
     float t;
-    int step;
-    float dmul;
+    int ctr;
     V3 hit;
     float mid;
-    V3 nplus, nrm;
-    int probe;
-    V3 color, acc, dir0;
+    V3 nrm;
+    V3 color;
     int chan, bounces;
     bool inside;
+    float time;    // RM2 samplePDF seed
     V3 fin;        // RM2 finalColor
     uint32_t wl;   // RM3 hero wavelength
     float power;   // RM3
     int phase;
 };
+template <bool HO> RMR_D V3& hitref(Lane& L) {
+    if constexpr (HO) return L.o;
+    else return L.hit;
+}
+template <bool HO> RMR_D const V3& hitref(const Lane& L) {
+    if constexpr (HO) return L.o;
+    else return L.hit;
+}
+template <int VAR, bool PROG> constexpr bool hit_in_origin() { return VAR != RMR_VARIANT_RM2 && !PROG; }
 
 // ------------------------------------------------------------------------------------------
 // RNG: rand(co), RM1:44-57 (chained fract(sin) hash, state randChange per invocation)
 // ------------------------------------------------------------------------------------------
-RMR_D float lrand(Lane& L, V2 co) {
-    co.x = fmaf(L.gxt, L.rc, co.x);
-    co.y = fmaf(L.gyt, L.rc, co.y);
+RMR_D float rand_step(float gxt, float gyt, float& rc, V2 co) {
+    co.x = fmaf(gxt, rc, co.x);
+    co.y = fmaf(gyt, rc, co.y);
     float dt = dot2(co, v2(12.9898f, 78.233f));
     float sn = modf_glsl(dt, 3.14f);
-    L.rc = fractf(det_sin(sn) * 43758.5453f);
-    return L.rc;
+    rc = fractf(det_sin(sn) * 43758.5453f);
+    return rc;
 }
+RMR_D float lrand(Lane& L, V2 co) { return rand_step(L.gxt, L.gyt, L.rc, co); }
 
 // randHemisphere, RM1:270-304
 RMR_D V3 hemisphere(Lane& L, V2 s1, V2 s2, V3 n) {
@@ -187,10 +204,14 @@ __device__ __noinline__ float obj_program(const KParams& P, int begin, int end, 
 // NP == 0: sphere/box scene of any size, software-pipelined scalar loads (prim j+1 in flight
 //          while prim j is evaluated);
 // NP < 0 : general scene (node programs, Mandelbulb) through the 48-byte rmr_prim rows.
+// opU(a, b) = a.x < b.x ? a : b with the reference's NaN behaviour as compiled by Mesa llvmpipe
+// (per component: distance = min ignoring NaN, id = ordered select; oracle/rmr_oracle.c o_map).
+// Same bits as the plain select for every non-NaN input; d.x never becomes NaN.
 RMR_D void opu(V2& d, float dj, float mid) {
-    const bool keep = d.x < dj;
-    d.x = keep ? d.x : dj;
-    d.y = keep ? d.y : mid;
+    const bool take_id = !(d.x < dj);
+    const bool take_d = d.x >= dj;
+    d.y = take_id ? mid : d.y;
+    d.x = take_d ? dj : d.x;
 }
 
 // One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
@@ -279,9 +300,10 @@ RMR_D float gray_ch(V3 c, int chan) {
 
 #define PH_DONE (-1)
 
+template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
     L.t = 0.0f;
-    L.step = 0;
+    L.ctr = 0;
     if (P.max_steps > 0) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
@@ -290,17 +312,17 @@ RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
     } else {
         L.t = P.max_dist;
         L.mid = -1.0f;
-        L.hit = vfma(L.d, L.t, L.o);
+        hitref<HO>(L) = vfma(L.d, L.t, L.o);
         L.phase = PH_MISS;
     }
 }
 
 // trace() prologue: o = eye, d = dir, per-variant throughput init (RM1:485-492, RM2:422-429,
 // RM3:349-355). Returns false if the trace has zero bounces (loop body never runs).
-template <int VAR>
-RMR_D bool trace_prologue(const KParams& P, Lane& L) {
+template <int VAR, bool HO>
+RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir) {
     L.o = v3(P.eye[0], P.eye[1], P.eye[2]);
-    L.d = L.dir0;
+    L.d = dir;
     L.bounces = 0;
     L.inside = false;
     if (VAR == RMR_VARIANT_RM1) L.color = channel_vec(L.chan);
@@ -308,18 +330,48 @@ RMR_D bool trace_prologue(const KParams& P, Lane& L) {
     if (VAR == RMR_VARIANT_RM3) { L.wl = 0u; L.power = 1.0f; }
     if (L.bounces < P.max_bounces) {
         L.bounces = 1;
-        L.dmul = 1.0f;
-        start_march(P, L, PH_MARCH);
+        start_march<HO>(P, L, PH_MARCH);
         return true;
     }
     return false;
 }
 
-// End of trace(): fold the channel result, start the next channel's trace (separateChannels,
-// RM1:586-598) or finish the sample. Returns true when the sample is complete (result in L.acc).
-template <int VAR>
+// unit -> (sample k, pixel); false if the pixel is outside the clip rect
+RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& time) {
+    const uint32_t per_k = (uint32_t)P.n_tiles * 64u;
+    const uint32_t k = u / per_k;
+    const uint32_t rem = u - k * per_k;
+    const int tile = (int)(rem >> 6), lane = (int)(rem & 63u);
+    const TileXY txy = P.tiles[tile];
+    px = txy.x + (lane & 7);
+    py = txy.y + (lane >> 3);
+    time = P.times[k];
+    return !(px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1);
+}
+
+// main(): jittered corner ray, RM1:569-584 (identical in RM2/RM3). The three rand() calls start
+// the invocation's chain (randChange = 0); `rc` returns the chain state after them.
+RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
+    const float gxt = (float)px + time, gyt = (float)py + time;
+    rc = 0.0f;
+    const float W = (float)P.W, H = (float)P.H;
+    const float posx = (float)px / W, posy = (float)py / H;
+    const float j1 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
+    const float j2 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
+    const float j3 = rand_step(gxt, gyt, rc, v2((float)py + time, (float)px + time));
+    const V3 r00 = v3(P.r00[0], P.r00[1], P.r00[2]), r01 = v3(P.r01[0], P.r01[1], P.r01[2]);
+    const V3 r10 = v3(P.r10[0], P.r10[1], P.r10[2]), r11 = v3(P.r11[0], P.r11[1], P.r11[2]);
+    const V3 top = vmix(r00, r01, posx + j1 / W);
+    const V3 bot = vmix(r10, r11, posx + j2 / W);
+    return normalize(vmix(top, bot, posy + j3 / H));
+}
+
+// End of trace(): store the channel result into the sample plane. Returns true when the sample
+// is complete; otherwise (separateChannels, RM1:586-598) the lane is parked in PH_RESTART and the
+// next channel's trace starts where new units start (one inlined copy of the ray setup).
+template <int VAR, bool HO>
 RMR_D bool finish_trace(const KParams& P, Lane& L) {
-    for (;;) {
+    {
         V3 res;
         if (VAR == RMR_VARIANT_RM1) res = L.color;
         if (VAR == RMR_VARIANT_RM2) {
@@ -340,73 +392,82 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
             else if (wl > 700.0f) alpha = (780.0f - wl) / 80.0f;
             else if (wl < 420.0f) alpha = (wl - 380.0f) / 40.0f;
             else alpha = 1.0f;
-            L.acc = (v3(R, G, B) * alpha) * L.power;
+            const V3 c = (v3(R, G, B) * alpha) * L.power;
+            P.samp[L.unit] = make_float4(c.x, c.y, c.z, 1.0f);
             return true;
         }
-        if (L.chan < 0) { L.acc = res; return true; }
-        L.acc = (L.chan == 0) ? res : L.acc + res;   // (r + g) + b, RM1:597
+        if (L.chan < 0) {
+            P.samp[L.unit] = make_float4(res.x, res.y, res.z, 1.0f);
+            return true;
+        }
+        // separateChannels: (r + g) + b, RM1:597; the partial sum lives in the sample plane
+        V3 acc = res;
+        if (L.chan != 0) {
+            const float4 pv = P.samp[L.unit];
+            acc = v3(pv.x, pv.y, pv.z) + res;
+        }
+        P.samp[L.unit] = make_float4(acc.x, acc.y, acc.z, 1.0f);
         if (L.chan == 2) return true;
         L.chan++;
-        if (trace_prologue<VAR>(P, L)) return false;
+        L.phase = PH_RESTART;
+        return false;
     }
 }
 
 // `while (bounces < maxBounces) { bounces++; v = march(o, d, ...) ...}`: next march or trace end
-template <int VAR>
+template <int VAR, bool HO>
 RMR_D void next_bounce(const KParams& P, Lane& L) {
     if (L.bounces < P.max_bounces) {
         L.bounces++;
-        L.dmul = L.inside ? -1.0f : 1.0f;
-        start_march(P, L, PH_MARCH);
-    } else if (finish_trace<VAR>(P, L)) {
+        start_march<HO>(P, L, PH_MARCH);   // march sign = inside ? -1 : 1
+    } else if (finish_trace<VAR, HO>(P, L)) {
         L.phase = PH_DONE;
     }
 }
 
 // main(): jittered corner ray, RM1:569-584 (identical in RM2/RM3)
-template <int VAR>
-RMR_D bool start_unit(const KParams& P, Lane& L, uint64_t u) {
-    const uint64_t per_k = (uint64_t)P.n_tiles * 64u;
-    const uint32_t k = (uint32_t)(u / per_k);
-    const uint32_t rem = (uint32_t)(u - (uint64_t)k * per_k);
-    const int tile = (int)(rem >> 6), lane = (int)(rem & 63u);
-    const TileXY txy = P.tiles[tile];
-    const int px = txy.x + (lane & 7), py = txy.y + (lane >> 3);
-    if (px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1) return false;
-    L.unit = u;
-    L.px = px; L.py = py;
-    const float time = P.times[k];
-    L.time = time;
-    L.gxt = (float)px + time;
-    L.gyt = (float)py + time;
-    L.rc = 0.0f;
-    const float W = (float)P.W, H = (float)P.H;
-    const float posx = (float)px / W, posy = (float)py / H;
-    const float j1 = lrand(L, v2((float)px + time, (float)py + time));
-    const float j2 = lrand(L, v2((float)px + time, (float)py + time));
-    const float j3 = lrand(L, v2((float)py + time, (float)px + time));
-    const V3 r00 = v3(P.r00[0], P.r00[1], P.r00[2]), r01 = v3(P.r01[0], P.r01[1], P.r01[2]);
-    const V3 r10 = v3(P.r10[0], P.r10[1], P.r10[2]), r11 = v3(P.r11[0], P.r11[1], P.r11[2]);
-    const V3 top = vmix(r00, r01, posx + j1 / W);
-    const V3 bot = vmix(r10, r11, posx + j2 / W);
-    L.dir0 = normalize(vmix(top, bot, posy + j3 / H));
-    L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
-    L.acc = v3s(0.0f);
-    if (!trace_prologue<VAR>(P, L) && finish_trace<VAR>(P, L)) L.phase = PH_DONE;
-    return true;
+// (Re)start a trace: a fresh unit (fresh = true: pixel, seed chain, channel) or the next
+// separateChannels pass of this lane's unit (same primary ray; the rand chain continues).
+template <int VAR, bool HO>
+RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
+    int px, py;
+    float time, rc;
+    const bool in_rect = unit_pixel(P, u, px, py, time);
+    if (fresh && !in_rect) {
+        L.phase = PH_IDLE;
+        return;
+    }
+    const V3 dir = primary_dir(P, px, py, time, rc);
+    if (fresh) {
+        L.unit = u;
+        L.time = time;
+        L.gxt = (float)px + time;
+        L.gyt = (float)py + time;
+        L.rc = rc;
+        L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
+    }
+    for (;;) {  // a zero-bounce trace finishes at once (and may start the next channel)
+        if (trace_prologue<VAR, HO>(P, L, dir)) return;
+        if (finish_trace<VAR, HO>(P, L)) {
+            L.phase = PH_DONE;
+            return;
+        }
+    }
 }
 
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
+// distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
+template <bool HO>
 RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
     const bool shadow = (L.phase == PH_SHADOW);
-    const float dist = m.x * (shadow ? 1.0f : L.dmul);
+    const float dist = (L.inside && !shadow) ? -m.x : m.x;
     if (dist < 0.001f) {
         if (shadow) {          // sd = t; keep hit/mid/normal of the shaded point
             L.phase = PH_NEE;
         } else {
             L.mid = m.y;
-            L.hit = vfma(L.d, L.t, L.o);
-            L.probe = 0;
+            hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            L.ctr = 0;
             L.phase = PH_NORMAL;
         }
         return;
@@ -414,8 +475,8 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
     bool miss = L.t >= P.max_dist;
     if (!miss) {
         L.t = fmaf(dist, P.step_mult, L.t);
-        L.step++;
-        miss = (L.step >= P.max_steps);
+        L.ctr++;
+        miss = (L.ctr >= P.max_steps);
     }
     if (miss) {
         L.t = P.max_dist;
@@ -423,7 +484,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
             L.phase = PH_NEE;
         } else {
             L.mid = -1.0f;
-            L.hit = vfma(L.d, L.t, L.o);
+            hitref<HO>(L) = vfma(L.d, L.t, L.o);
             L.phase = PH_MISS;
         }
     }
@@ -432,24 +493,26 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
 // getNormal probe order: +x, -x, +y, -y, +z, -z (RM1:263-265).
 // +probes add (+h, +0, +0); -probes add (-h, -0, -0): x + (-0) == x - 0 bit for bit, so this is
 // exactly the oracle's p +- vec3(h,0,0) without a divergent switch (A/B: +10% vs a switch).
+template <bool HO>
 RMR_D V3 probe_point(const Lane& L) {
     const float h = 0.001f;
-    const int ax = L.probe >> 1;
-    const bool neg = (L.probe & 1) != 0;
+    const int ax = L.ctr >> 1;
+    const bool neg = (L.ctr & 1) != 0;
     const float hs = neg ? -h : h, z0 = neg ? -0.0f : 0.0f;
-    return v3(L.hit.x + (ax == 0 ? hs : z0), L.hit.y + (ax == 1 ? hs : z0), L.hit.z + (ax == 2 ? hs : z0));
+    const V3 hp = hitref<HO>(L);
+    return v3(hp.x + (ax == 0 ? hs : z0), hp.y + (ax == 1 ? hs : z0), hp.z + (ax == 2 ? hs : z0));
 }
+// nrm.c holds map(p + h e_c) after the + probe and map(p + h e_c) - map(p - h e_c) after the - probe
 RMR_D void normal_update(Lane& L, float m) {
-    const int ax = L.probe >> 1;
-    const bool plus = (L.probe & 1) == 0;
-    L.nplus.x = (plus && ax == 0) ? m : L.nplus.x;
-    L.nplus.y = (plus && ax == 1) ? m : L.nplus.y;
-    L.nplus.z = (plus && ax == 2) ? m : L.nplus.z;
-    L.nrm.x = (!plus && ax == 0) ? L.nplus.x - m : L.nrm.x;
-    L.nrm.y = (!plus && ax == 1) ? L.nplus.y - m : L.nrm.y;
-    L.nrm.z = (!plus && ax == 2) ? L.nplus.z - m : L.nrm.z;
-    L.probe++;
-    if (L.probe == 6) {
+    const int ax = L.ctr >> 1;
+    const bool plus = (L.ctr & 1) == 0;
+    // (no select between struct fields here: clang turns that into a dynamic stack index)
+    const float vx = plus ? m : L.nrm.x - m, vy = plus ? m : L.nrm.y - m, vz = plus ? m : L.nrm.z - m;
+    L.nrm.x = ax == 0 ? vx : L.nrm.x;
+    L.nrm.y = ax == 1 ? vy : L.nrm.y;
+    L.nrm.z = ax == 2 ? vz : L.nrm.z;
+    L.ctr++;
+    if (L.ctr == 6) {
         L.nrm = normalize(L.nrm);
         L.phase = PH_HIT;
     }
@@ -573,18 +636,19 @@ RMR_D void run_material_v1(const KParams& P, Lane& L, int m, V3& oc, V3& od, V3&
 }
 
 // trace() hit tail, RM1:526-553
+template <bool HO>
 RMR_D void rm1_after_material(const KParams& P, Lane& L, V3 nc, V3 nd, V3 ni, V3 nh) {
     L.color = L.color * nc;
     L.inside = ni.x != 0.0f;
     if (is_zero(nd)) {
-        if (finish_trace<RMR_VARIANT_RM1>(P, L)) L.phase = PH_DONE;
+        if (finish_trace<RMR_VARIANT_RM1, HO>(P, L)) L.phase = PH_DONE;
         return;
     }
-    const V3 hit = L.hit;
+    const V3 hit = hitref<HO>(L);
     L.d = nd;
     if (is_zero(nh)) L.o = L.inside ? vfma(L.nrm, -0.002f, hit) : vfma(L.nrm, 0.003f, hit);
     else L.o = nh;
-    next_bounce<RMR_VARIANT_RM1>(P, L);
+    next_bounce<RMR_VARIANT_RM1, HO>(P, L);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -681,6 +745,7 @@ RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) 
 // ------------------------------------------------------------------------------------------
 template <int VAR, bool PROG>
 RMR_D void shade(const KParams& P, Lane& L) {
+    constexpr bool HO = hit_in_origin<VAR, PROG>();
     if (VAR == RMR_VARIANT_RM1) {
         const bool want = (L.phase == PH_HIT);
         const int id = want ? (int)L.mid : -1;
@@ -693,7 +758,8 @@ RMR_D void shade(const KParams& P, Lane& L) {
         V3 nc = v3s(0.0f), nd = v3s(0.0f), ni = v3s(0.0f), nh = v3s(0.0f);
         if (kind == MAT_DIFFUSE) {          // shader_diffuse(ray, c, color, dir), RM1:378-387
             nc = v3(dm.c[0], dm.c[1], dm.c[2]);
-            nd = hemisphere(L, v2(L.hit.x, L.hit.y), v2(L.hit.z, L.hit.x), L.nrm);
+            const V3 hp = hitref<HO>(L);
+            nd = hemisphere(L, v2(hp.x, hp.y), v2(hp.z, hp.x), L.nrm);
         } else if (kind == MAT_EMISSION) {  // shader_emission(ray, c, p, color), RM1:476-479
             nc = v3(dm.c[0], dm.c[1], dm.c[2]) * gray_ch(v3(dm.p[0], dm.p[1], dm.p[2]) * channel_vec(L.chan), L.chan);
         }
@@ -708,17 +774,17 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 pending &= ~__ballot(mine);
             }
         }
-        if (want) rm1_after_material(P, L, nc, nd, ni, nh);
+        if (want) rm1_after_material<HO>(P, L, nc, nd, ni, nh);
         if (L.phase == PH_MISS) {  // shader_emission(ray, skyColor(dir), vec3(1), emit), RM1:555-561
             const V3 emit = v3(P.sky[0], P.sky[1], P.sky[2]) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
             L.color = L.color * emit;
-            if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
     }
     if (VAR == RMR_VARIANT_RM2) {
         const V3 lp = v3(P.rm2_light[0], P.rm2_light[1], P.rm2_light[2]);
         if (L.phase == PH_HIT) {  // RM2:436-506
-            const V3 pos = L.hit, N = L.nrm, pdir = -L.d;
+            const V3 pos = hitref<HO>(L), N = L.nrm, pdir = -L.d;
             const int id = (int)L.mid;
             if (id == P.rm2_node_id) {
                 V3 t0, t1, t2;
@@ -729,19 +795,19 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 L.color = L.color * matc;
                 if (wb) {
                     L.color = v3s(0.0f);
-                    if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+                    if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
                 } else {
                     L.o = vfma(N, 0.002f, pos);
                     L.d = nd;
-                    next_bounce<VAR>(P, L);
+                    next_bounce<VAR, HO>(P, L);
                 }
             } else {  // light-march toward the point light, RM2:481
                 L.o = vfma(N, 0.002f, pos);
                 L.d = normalize(lp - pos);
-                start_march(P, L, PH_SHADOW);   // hit/mid/nrm stay for the NEE step
+                start_march<HO>(P, L, PH_SHADOW);   // hit/mid/nrm stay for the NEE step
             }
         } else if (L.phase == PH_NEE) {  // RM2:482-501
-            const V3 pos = L.hit, N = L.nrm;
+            const V3 pos = hitref<HO>(L), N = L.nrm;
             const float sd = L.t;
             const V3 mc = rm2_albedo(P, (int)L.mid);
             const V3 ld = normalize(lp - pos);
@@ -761,19 +827,19 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 L.color = L.color * (mc / v3s(prob));
                 L.o = vfma(N, 0.002f, pos);
                 L.d = nd;
-                next_bounce<VAR>(P, L);
+                next_bounce<VAR, HO>(P, L);
             } else {
                 L.color = v3s(0.0f);
-                if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+                if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
             }
         } else if (L.phase == PH_MISS) {
             L.color = L.color * v3(P.sky[0], P.sky[1], P.sky[2]);
-            if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
     }
     if (VAR == RMR_VARIANT_RM3) {
         if (L.phase == PH_HIT) {  // RM3:368-406
-            const V3 pos = L.hit, N = L.nrm;
+            const V3 pos = hitref<HO>(L), N = L.nrm;
             const int id = (int)L.mid;
             V3 nd = v3s(0.0f);
             bool stop = false;
@@ -784,16 +850,16 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 else nd = hemisphere(L, v2(pos.x, pos.y), v2(pos.z, pos.y), N);
             }
             if (stop) {
-                if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+                if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
             } else {
                 L.o = vfma(N, 0.002f, pos);
                 L.d = nd;
-                next_bounce<VAR>(P, L);
+                next_bounce<VAR, HO>(P, L);
             }
         } else if (L.phase == PH_MISS) {  // RM3:408-438
-            const V3 pos = L.hit;
+            const V3 pos = hitref<HO>(L);
             spectral_event(L, P.spec_sky.min_wave, P.spec_sky.max_wave, P.spec_sky.power, v2(pos.y, pos.x));
-            if (finish_trace<VAR>(P, L)) L.phase = PH_DONE;
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
     }
 }
@@ -807,56 +873,66 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 // Occupancy target (waves per SIMD) for the fast specialisations: the kernel is latency-bound
 // (scalar-load and dependent-chain stalls), and 8 waves/SIMD measured +8% over the 5 that the
 // register allocator picks unconstrained. The general/interpreter kernels keep their registers.
+#ifndef RMR_FAST_WAVES
+#define RMR_FAST_WAVES 8
+#endif
 template <int VAR, int NP, bool PERSIST, bool PROG>
-__global__ __launch_bounds__(256, ((NP < 0 || PROG || VAR == RMR_VARIANT_RM2) ? 1 : 8)) void k_trace(KParams P) {
+__global__ __launch_bounds__(256, ((NP < 0 || PROG || VAR == RMR_VARIANT_RM2) ? 1 : RMR_FAST_WAVES)) void k_trace(KParams P) {
+    constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
     uint64_t maps = 0, iters = 0, shades = 0;
-    constexpr uint64_t CHUNK = 128;
-    uint64_t rnext = 0, rend = 0;
+    constexpr uint32_t CHUNK = 128;
+    const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
+    uint32_t rnext = 0, rend = 0;
     bool exhausted = false;
     if (!PERSIST) {
-        const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (u < P.n_units) {
-            if (!start_unit<VAR>(P, L, u)) L.phase = PH_IDLE;
-        }
+        const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+        if (u < n_units) begin_trace<VAR, HO>(P, L, u, true);
         exhausted = true;
     }
     const int T = P.shade_threshold;
     for (;;) {
+        bool fresh = false;
+        uint32_t fu = 0;
         if (PERSIST && !exhausted) {
             uint64_t idle = __ballot(L.phase == PH_IDLE);
             uint64_t act0 = __ballot(is_active(L.phase));
             if (idle && (__popcll(idle) >= T || act0 == 0)) {
                 if (rnext >= rend) {
-                    unsigned long long base = 0;
-                    if (__lane_id() == 0) base = atomicAdd(P.queue, (unsigned long long)CHUNK);
-                    base = __shfl(base, 0);
+                    unsigned int base = 0;
+                    if (__lane_id() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK);
+                    base = __builtin_amdgcn_readfirstlane(base);
                     rnext = base;
-                    rend = base + CHUNK < P.n_units ? base + CHUNK : P.n_units;
-                    if (base >= P.n_units) exhausted = true;
+                    exhausted = base >= n_units;
+                    rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
                 }
                 if (!exhausted) {
-                    const uint64_t avail = rend - rnext;
+                    const uint32_t avail = rend - rnext;
                     const uint32_t nidle = (uint32_t)__popcll(idle);
-                    const uint64_t take = avail < nidle ? avail : nidle;
+                    const uint32_t take = avail < nidle ? avail : nidle;
                     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     if (L.phase == PH_IDLE && rank < take) {
-                        if (!start_unit<VAR>(P, L, rnext + rank)) L.phase = PH_IDLE;
+                        fresh = true;
+                        fu = rnext + rank;
                     }
                     rnext += take;
                 }
             }
         }
+        const bool restart = (L.phase == PH_RESTART);
+        if (__ballot(fresh || restart)) {
+            if (fresh || restart) begin_trace<VAR, HO>(P, L, fresh ? fu : L.unit, fresh);
+        }
         const bool act = is_active(L.phase);
         const uint64_t amask = __ballot(act);
         if (amask) {
             if (act) {
-                const V3 p = (L.phase == PH_NORMAL) ? probe_point(L) : vfma(L.d, L.t, L.o);
+                const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
                 const V2 m = scene_map<NP>(P, p);
                 if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                else march_update(P, L, m);
+                else march_update<HO>(P, L, m);
             }
             maps += (uint64_t)__popcll(amask);
             iters++;
@@ -866,16 +942,9 @@ __global__ __launch_bounds__(256, ((NP < 0 || PROG || VAR == RMR_VARIANT_RM2) ? 
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
             if (is_shade(L.phase)) shade<VAR, PROG>(P, L);
-            if (L.phase == PH_DONE) {
-                P.samp[L.unit] = make_float4(L.acc.x, L.acc.y, L.acc.z, 1.0f);
-                L.phase = PH_IDLE;
-            }
         }
-        // samples that completed outside the shade block (bounce limit reached in next_bounce)
-        if (L.phase == PH_DONE) {
-            P.samp[L.unit] = make_float4(L.acc.x, L.acc.y, L.acc.z, 1.0f);
-            L.phase = PH_IDLE;
-        }
+        // finished samples have stored their radiance (finish_trace): the lane is free
+        if (L.phase == PH_DONE) L.phase = PH_IDLE;
         const uint64_t live = __ballot(L.phase != PH_IDLE);
         if (live == 0 && exhausted) break;
     }

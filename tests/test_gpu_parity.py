@@ -30,6 +30,8 @@ CASES = [
     ("rm1_sphere1_b1", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 1}),
     ("rm1_default_sepch", os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {"separate_channels": 1}),
     ("rm1_cornell5_steps", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 3, "max_steps": 40}),
+    ("rm1_mandelbulb_b2", os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}),
+    ("rm1_csg256_b4", os.path.join(SCENES, "csg256.scene"), "rm1", {"max_bounces": 4}),
 ]
 
 

@@ -53,6 +53,21 @@ def test_kat_normal(name):
     assert np.abs(out - k["normal_out"][hit]).max() <= 1e-4
 
 
+@pytest.mark.parametrize("name", ["cornell5", "default"])
+def test_kat_nan_direction_semantics(name):
+    """A NaN ray direction (normalize(vec3(0)) after total internal reflection) on the reference:
+    map(NaN) and march(o, NaN, +-1) as llvmpipe evaluates them (opU per component, see o_map)."""
+    k = np.load(os.path.join(GOLDEN, "kat_nan.npz"))
+    t = _tables(*KATS[name])
+    nan3 = np.full(3, np.nan, np.float32)
+    ref = k["%s_out" % name]
+    for o, r in zip(k["%s_origin" % name], ref):
+        m = oracle.map_p(t, nan3)
+        a = oracle.march(t, o, nan3, 1.0)
+        b = oracle.march(t, o, nan3, -1.0)
+        np.testing.assert_array_equal(np.concatenate([m, a, b]), r)
+
+
 def test_kat_wavelength_to_color_exact():
     k = np.load(os.path.join(GOLDEN, "kat_rm3.npz"))
     out = np.array([oracle.wl2rgb(int(w)) for w in k["wl_in"]])
