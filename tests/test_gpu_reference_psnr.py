@@ -7,6 +7,10 @@ values, and for large seeds on the driver's float32 sin() rounding (at time ~ 40
 implementations' Cornell-5 means differ by 8.7%), so a converged image is only comparable on a
 shared, small-seed schedule. The two streams are still independent (the hash is chaotic), so PSNR is
 bounded by both sides' Monte-Carlo noise. PSNR is over linear RGB clamped to [0, 1].
+
+Round-1 results (MI355X): Cornell-5 45.4 dB, default 43.1, glass 46.7, multilight 44.8, sphere 63.8,
+RM2 simple 102.4, RM3 51.6; |mean difference| <= 0.45 %. Scenes with refraction need the reference's
+NaN behaviour of opU (see oracle/rmr_oracle.c o_map): without it default.scene is at 23.5 dB.
 """
 import os
 
@@ -25,9 +29,9 @@ CASES = {
     "rm1_cornell5_b4": (os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 4}, 40.0),
     "rm1_sphere1_b1": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 1}, 40.0),
     "rm2_simple": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {}, 40.0),
-    "rm1_glass": (os.path.join(GOLDEN, "scenes", "glass_test.scene"), "rm1", {}, 35.0),
-    "rm1_multilight": (os.path.join(GOLDEN, "scenes", "multilight.scene"), "rm1", {}, 35.0),
-    "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}, 35.0),
+    "rm1_glass": (os.path.join(GOLDEN, "scenes", "glass_test.scene"), "rm1", {}, 40.0),
+    "rm1_multilight": (os.path.join(GOLDEN, "scenes", "multilight.scene"), "rm1", {}, 40.0),
+    "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}, 40.0),
 }
 
 
@@ -59,4 +63,4 @@ def test_converged_psnr_vs_reference(renderer, name):
     rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(ref[..., :3].mean(), 1e-12)
     print("%s: PSNR %.2f dB vs reference @%d spp (GPU %d spp), mean rel diff %+.4f" % (name, p, n_ref, n, rel))
     assert p >= floor
-    assert abs(rel) < 0.02
+    assert abs(rel) < 0.01
