@@ -54,6 +54,7 @@ typedef struct rmr_stats {
     double   flops_per_map;  /* algorithmic flops of one map() for the loaded scene            */
     uint64_t map_iters;      /* wave-level map() iterations: map_evals/(64*map_iters) = lane use */
     uint64_t shade_batches;  /* wave-level deferred-shading batches                             */
+    uint64_t jit_launches;   /* trace launches that ran the hipRTC scene-specialised kernel     */
 } rmr_stats;
 
 /* ---- lifetime --------------------------------------------------------------------------- */
@@ -148,11 +149,27 @@ int rmr_load_accum(rmr_ctx* ctx, const char* path, uint32_t* samples_done);
 int rmr_sync(rmr_ctx* ctx);
 int rmr_get_stats(rmr_ctx* ctx, rmr_stats* out);
 int rmr_reset_stats(rmr_ctx* ctx);
+/* Profiling builds only (librmr compiled with -DRMR_PROFILE; zeros otherwise): per-wave shader-clock
+ * cycles summed over all waves since rmr_reset_stats, split into [0] refill/ray setup, [1] map()
+ * iterations, [2] shading batches, [3] whole trace loop. */
+int rmr_get_section_cycles(rmr_ctx* ctx, uint64_t out[4]);
 /* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */
 int rmr_set_kernel(rmr_ctx* ctx, int kernel);
+/* Per-scene kernel specialisation (the reference recompiles its shader per scene, Graphics::Reload):
+ * the scene's map() is generated as HIP source with the primitives as literals and compiled by
+ * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under
+ * $RMR_JIT_CACHE or ~/.cache/rmr-jit). Results are bit-identical to the table-driven kernels.
+ * mode 0 = off, 1 = always (errors are returned), 2 = auto (default: launches of >= 2^20 units;
+ * a failed compile falls back to the table-driven kernel). Env RMR_JIT overrides at rmr_create. */
+int rmr_set_jit(rmr_ctx* ctx, int mode);
+/* Compile the specialised kernel of a scene without a GPU (json NULL = the variant's built-in
+ * scene). On success `log` receives the code-object key, otherwise the compiler log. */
+int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);
 /* Tuning knobs (<= 0 / < 0 keeps the current value): deferred-shading batch size in lanes (1..64),
  * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. */
 int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long samp_budget_bytes);
+/* (shade_threshold bits 8..15, when non-zero, set the refill threshold separately: idle lanes a
+ * wave collects before it fetches new units; default = the shading threshold.) */
 /* Test hook: per-sample radiance (before the running mean) of the integer rect, written as
  * out[k][y-y0][x-x0][4]; sample k is seeded with times[k]. The accumulator is left unchanged. */
 int rmr_trace_samples(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out);

@@ -18,7 +18,15 @@
 #ifndef RMR_TABLES_H
 #define RMR_TABLES_H
 
+#ifdef __HIPCC_RTC__ /* hipRTC (per-scene kernel specialisation) has no <stdint.h> */
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::uint8_t uint8_t;
+#else
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -104,4 +104,4 @@ def default_params(**kw):
 class Stats(C.Structure):
     _fields_ = [("map_evals", C.c_uint64), ("samples", C.c_uint64), ("trace_launches", C.c_uint64),
                 ("trace_ms", C.c_double), ("fold_ms", C.c_double), ("flops_per_map", C.c_double),
-                ("map_iters", C.c_uint64), ("shade_batches", C.c_uint64)]
+                ("map_iters", C.c_uint64), ("shade_batches", C.c_uint64), ("jit_launches", C.c_uint64)]

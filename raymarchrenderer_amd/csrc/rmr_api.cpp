@@ -19,6 +19,7 @@
 
 #include "../../include/rmr.h"
 #include "rmr_internal.h"
+#include "rmr_jit.hpp"
 #include "scene.hpp"
 
 namespace rmr {
@@ -72,8 +73,17 @@ struct rmr_ctx {
     std::vector<EventPair> pending, pool;
     rmr_stats stats{};
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
-    int shade_threshold = 10;
+    int shade_threshold = 16;
+    int refill_threshold = 8;   // 0 = shade_threshold (tuned on C2: T=16, refill at 8 idle lanes)
     int grid_per_cu = 0;  // 0 = occupancy
+    // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
+    // >= jit_min_units units; smaller renders use the ahead-of-time kernels)
+    int jit_mode = 2;
+    uint64_t jit_min_units = (uint64_t)1 << 20;
+    bool jit_ready = false;     // `jit` matches the loaded scene
+    bool jit_failed = false;    // compile/load failed for the loaded scene (auto mode falls back)
+    rmr::JitKernel jit;
+    std::vector<rmr::JitKernel> jit_loaded;  // modules loaded by this context (unloaded at destroy)
     size_t samp_budget = (size_t)8 << 30;
     std::string err;
 };
@@ -172,7 +182,39 @@ int upload_scene(rmr_ctx* c) {
     for (const auto& d : dm) c->has_prog = c->has_prog || d.kind == rmr::MAT_PROGRAM;
     if ((r = dev_upload(c, &c->d_dmats, dm.data(), dm.size()))) return r;
     c->scene_loaded = true;
+    c->jit_ready = false;
+    c->jit_failed = false;
     c->stats.flops_per_map = s.flops_per_map();
+    return RMR_OK;
+}
+
+// Compile (or fetch from the cache) and load the specialised trace kernel of the loaded scene.
+int ensure_jit(rmr_ctx* c) {
+    if (c->jit_ready) return RMR_OK;
+    const std::string src = rmr::jit_source(c->scene, c->has_prog);
+    std::vector<char> code;
+    std::string key, log;
+    if (!rmr::jit_compile(src, code, key, log)) {
+        c->jit_failed = true;
+        return fail(c, RMR_E_HIP, "hipRTC specialisation failed: " + log.substr(0, 2000));
+    }
+    for (const auto& k : c->jit_loaded) {
+        if (k.key == key) {
+            c->jit = k;
+            c->jit_ready = true;
+            return RMR_OK;
+        }
+    }
+    rmr::JitKernel k;
+    k.key = key;
+    HIPCHK(c, hipModuleLoadData(&k.module, code.data()));
+    HIPCHK(c, hipModuleGetFunction(&k.fn, k.module, "rmr_jit_trace"));
+    int b = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, 256, 0) != hipSuccess || b <= 0) b = 4;
+    k.blocks_per_cu = b;
+    c->jit_loaded.push_back(k);
+    c->jit = k;
+    c->jit_ready = true;
     return RMR_OK;
 }
 
@@ -308,10 +350,22 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.queue = c->d_queue;
     P.counters = c->d_counters;
     P.shade_threshold = c->shade_threshold;
+    P.refill_threshold = c->refill_threshold > 0 ? c->refill_threshold : c->shade_threshold;
 
+    // hipRTC specialisation for large launches (always when jit_mode == 1)
+    bool use_jit = false;
+    if (c->kernel_mode == 0 && c->jit_mode != 0 && !(c->jit_mode == 2 && c->jit_failed)) {
+        const uint64_t units = (uint64_t)std::min<size_t>(chunk, nspp) * plane;
+        if (c->jit_mode == 1 || units >= c->jit_min_units) {
+            const int jr = ensure_jit(c);
+            if (jr == RMR_OK) use_jit = true;
+            else if (c->jit_mode == 1) return jr;
+        }
+    }
     int bpc = c->grid_per_cu;
     if (bpc <= 0) {
-        if (rmr::trace_occupancy(s.variant, c->map_np, c->has_prog, &bpc) != 0 || bpc <= 0) bpc = 4;
+        if (use_jit) bpc = c->jit.blocks_per_cu;
+        else if (rmr::trace_occupancy(s.variant, c->map_np, c->has_prog, &bpc) != 0 || bpc <= 0) bpc = 4;
     }
     const int grid = c->n_cu * bpc;
     for (uint32_t k0 = 0; k0 < nspp; k0 += (uint32_t)chunk) {
@@ -323,7 +377,13 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(unsigned long long), c->stream));
         EventPair ev = get_events(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
-        HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
+        if (use_jit) {
+            void* args[] = {&P};
+            HIPCHK(c, hipModuleLaunchKernel(c->jit.fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+            c->stats.jit_launches++;
+        } else {
+            HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
+        }
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         HIPCHK(c, rmr::launch_fold(P, c->stream));
         HIPCHK(c, hipEventRecord(ev.c, c->stream));
@@ -380,13 +440,15 @@ int rmr_create(rmr_ctx** out, int device) {
     c->own_stream = true;
     rmr_default_params(&c->params);
     if (hipMalloc((void**)&c->d_queue, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         rmr_destroy(c);
         return RMR_E_HIP;
     }
     if (const char* e = std::getenv("RMR_SHADE_T")) c->shade_threshold = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RMR_REFILL_T")) c->refill_threshold = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
     *out = c;
     return RMR_OK;
@@ -403,6 +465,8 @@ void rmr_destroy(rmr_ctx* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
+    for (auto& k : c->jit_loaded)
+        if (k.module) (void)hipModuleUnload(k.module);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -651,6 +715,16 @@ int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
     return RMR_OK;
 }
 
+int rmr_get_section_cycles(rmr_ctx* c, uint64_t out[4]) {
+    if (!c || !out) return RMR_E_INVALID;
+    int r = rmr_sync(c);
+    if (r) return r;
+    unsigned long long cnt[8];
+    HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; i++) out[i] = cnt[4 + i];
+    return RMR_OK;
+}
+
 int rmr_reset_stats(rmr_ctx* c) {
     if (!c) return RMR_E_INVALID;
     int r = rmr_sync(c);
@@ -658,7 +732,7 @@ int rmr_reset_stats(rmr_ctx* c) {
     const double fpm = c->stats.flops_per_map;
     c->stats = rmr_stats{};
     c->stats.flops_per_map = fpm;
-    HIPCHK(c, hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)));
     return RMR_OK;
 }
 
@@ -668,9 +742,43 @@ int rmr_set_kernel(rmr_ctx* c, int kernel) {
     return RMR_OK;
 }
 
+int rmr_set_jit(rmr_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 2) return RMR_E_INVALID;
+    c->jit_mode = mode;
+    c->jit_failed = false;
+    return RMR_OK;
+}
+
+int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen) {
+    std::string lg;
+    try {
+        CompiledScene s = (json && len) ? rmr::compile_scene(std::string(json, len), variant) : rmr::builtin_scene(variant);
+        bool prog = false;  // same rule as upload_scene: any RM1 material that is not a fast kind
+        if (s.variant == RMR_VARIANT_RM1) {
+            for (const auto& m : s.materials) {
+                if (!m.defined) continue;
+                const bool single = m.prog_end - m.prog_begin == 1 && m.inside_var < 0 && m.hit_var < 0;
+                const int code = single ? s.ops[(size_t)m.prog_begin].code : -1;
+                if (!(code == RMR_OP_M_DIFFUSE || code == RMR_OP_M_EMISSION)) prog = true;
+            }
+        }
+        std::vector<char> code;
+        std::string key;
+        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog), code, key, lg);
+        if (log && loglen) std::snprintf(log, loglen, "%s", ok ? key.c_str() : lg.c_str());
+        return ok ? RMR_OK : RMR_E_HIP;
+    } catch (const std::exception& e) {
+        if (log && loglen) std::snprintf(log, loglen, "%s", e.what());
+        return RMR_E_SCENE;
+    }
+}
+
 int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long samp_budget_bytes) {
     if (!c) return RMR_E_INVALID;
-    if (shade_threshold > 0) c->shade_threshold = std::min(64, shade_threshold);
+    if (shade_threshold > 0) {
+        c->shade_threshold = std::max(1, std::min(64, shade_threshold & 0xff));
+        c->refill_threshold = std::min(64, (shade_threshold >> 8) & 0xff);
+    }
     if (grid_per_cu >= 0) c->grid_per_cu = grid_per_cu;
     if (samp_budget_bytes > 0) c->samp_budget = (size_t)samp_budget_bytes;
     return RMR_OK;

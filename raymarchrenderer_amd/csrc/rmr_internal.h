@@ -1,6 +1,8 @@
 // rmr_internal.h — kernel launch parameters shared by the host API (rmr_api.cpp) and the kernels.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#endif
 #include "../../include/rmr_tables.h"
 
 namespace rmr {
@@ -68,6 +70,7 @@ struct KParams {
     unsigned long long* queue;  // persistent work counter
     unsigned long long* counters; // [0] map evals, [1] samples traced
     int32_t shade_threshold;    // deferred-shading batch size (lanes)
+    int32_t refill_threshold;   // idle lanes before a wave fetches new units
 };
 
 }  // namespace rmr

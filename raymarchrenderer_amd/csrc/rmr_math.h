@@ -8,8 +8,16 @@
 // sqrt and '/' are the correctly rounded IEEE operations (hipcc's default lowering), which is what
 // makes a bit-exact CPU restatement possible.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else  // hipRTC (per-scene specialisation, rmr_jit.cpp): no <stdint.h>
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::uint8_t uint8_t;
+#endif
 
 namespace rmr {
 
@@ -35,7 +43,25 @@ RMR_D bool is_zero(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
 RMR_D bool veq(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 RMR_D float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
 RMR_D float dot2(V2 a, V2 b) { return fmaf(a.x, b.x, a.y * b.y); }
-RMR_D float length(V3 a) { return sqrtf(dot(a, a)); }
+// Correctly rounded sqrt, bit-identical to sqrtf() for every input: v_sqrt_f32 (<= 1 ulp) plus the
+// one-ulp fixup (as hipcc's own lowering), without its denormal scaling and class check, which only
+// matter for 0 < x < 2^-96 — that rare range (and x < 0) takes a divergent branch to sqrtf(); +-0, inf
+// and NaN come out of the fast path unchanged. Verified exhaustively (tools/probes/sqrt_exhaustive.hip).
+RMR_D float sqrt_cr(float x) {
+#ifdef RMR_PLAIN_SQRT
+    return sqrtf(x);
+#else
+    const float s0 = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s0) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s0) + 1u);
+    const float rm = fmaf(-sm, s0, x), rp = fmaf(-sp, s0, x);
+    float s = (rm <= 0.0f) ? sm : s0;
+    s = (rp > 0.0f) ? sp : s;
+    if (__builtin_expect(x < 0x1p-96f && x != 0.0f, 0)) s = sqrtf(x);  // tiny or negative (not +-0, NaN)
+    return s;
+#endif
+}
+RMR_D float length(V3 a) { return sqrt_cr(dot(a, a)); }
 RMR_D V3 normalize(V3 a) { float inv = 1.0f / length(a); return a * inv; }
 RMR_D V3 vfma(V3 a, float s, V3 b) { return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z)); }
 RMR_D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
@@ -54,7 +80,7 @@ RMR_D V3 refract(V3 I, V3 N, float eta) {
     float d = dot(N, I);
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return v3s(0.0f);
-    float m = eta * d + sqrtf(k);
+    float m = eta * d + sqrt_cr(k);
     return v3(eta * I.x - m * N.x, eta * I.y - m * N.y, eta * I.z - m * N.z);
 }
 RMR_D float pow2(float x) { return x * x; }
@@ -120,12 +146,12 @@ RMR_D float det_acos(float x) {
     }
     if (hx >> 31) {
         float z = (1.0f + x) * 0.5f;
-        float s = sqrtf(z);
+        float s = sqrt_cr(z);
         float w = acos_R(z) * s - pio2_lo;
         return 2.0f * (pio2_hi - (s + w));
     }
     float z = (1.0f - x) * 0.5f;
-    float s = sqrtf(z);
+    float s = sqrt_cr(z);
     float df = __uint_as_float(__float_as_uint(s) & 0xfffff000u);
     float c = (z - df * df) / (s + df);
     float w = acos_R(z) * s + c;
@@ -205,21 +231,4 @@ RMR_D float det_atan2(float y, float x) {
 
 }  // namespace rmr
 
-namespace rmr {
-// Correctly rounded sqrt for x == 0 or x >= 2^-96 (and NaN): v_sqrt_f32 (<= 1 ulp) + the one-ulp
-// fix-up of hipcc's IEEE lowering, without its tiny-input rescaling. `tiny` is raised for
-// 0 < x < 2^-96, where the caller must redo the computation with sqrtf(). Verified exhaustively
-// against sqrtf on gfx950 (tools/probes/sqrt_exhaustive.hip).
-RMR_D float sqrt_cr_fast(float x, bool& tiny) {
-    tiny = tiny || (x < 0x1p-96f && x > 0.0f);
-    float s = __builtin_amdgcn_sqrtf(x);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
-    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
-    const float rm = fmaf(-sm, s, x);
-    const float rp = fmaf(-sp, s, x);
-    s = (rm <= 0.0f) ? sm : s;
-    s = (rp > 0.0f) ? sp : s;
-    return s;
-}
-RMR_D float length_fast(V3 a, bool& tiny) { return sqrt_cr_fast(dot(a, a), tiny); }
-}  // namespace rmr
+

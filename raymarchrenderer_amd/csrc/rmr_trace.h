@@ -1,0 +1,1032 @@
+// rmr_trace.h — device code of the rmr SDF ray-march path tracer (gfx950). Included by the
+// ahead-of-time build (rmr_kernels.hip) and, as an embedded string, by the per-scene hipRTC
+// specialisation (rmr_jit.cpp), which supplies its own map() with the scene baked in.
+//
+// Hot path of RayMarch.glsl / RayMarch2.glsl / RayMarch3.glsl ("RM1/RM2/RM3", under
+// /root/reference/RayMarch Renderer/): main -> trace -> march -> map, re-designed for CDNA4:
+//
+//  * k_trace<VARIANT, PERSIST>: one wave64 = 64 independent path states ("lanes"). Every loop
+//    iteration evaluates the scene SDF map() ONCE for every lane that needs one — a march step
+//    (RM1:233-257), a getNormal probe (RM1:259-268, its 6 map() calls become 6 iterations) or an
+//    RM2 shadow-march step (RM2:481) — so the expensive, wave-uniform prim loop always runs with
+//    as many lanes as possible. Lanes that reach a hit/miss park in a SHADE phase; shading (node
+//    materials, RNG, bounce logic) runs for the parked lanes in batches once enough of them wait
+//    (wave ballot). Finished lanes are refilled from a global atomic unit counter by ballot +
+//    mbcnt prefix ranks (PERSIST), so a wave never idles on its longest path.
+//  * Scene tables are read through the constant address space: the prim loop index is
+//    wave-uniform, so each prim is an s_load into SGPRs (no VGPR/LDS traffic in the hot loop).
+//  * A unit = (sample k, 8x8 tile, lane). Each path's radiance is written once, coalesced, to a
+//    per-sample plane samp[k][tile][64]; k_fold then applies the reference's FP32 running mean
+//    (RM1:600-612) in sample order, so the result equals nspp Graphics::Render calls bit for bit.
+//
+// Float semantics: rmr_math.h (compiled with -ffp-contract=off). All per-lane RNG call orders
+// follow the GLSL exactly; the CPU oracle (oracle/rmr_oracle.c) is the bitwise checker.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+#include "rmr_math.h"
+#include "rmr_internal.h"
+
+namespace rmr {
+
+typedef const __attribute__((address_space(4))) rmr_prim CPrim;
+typedef const __attribute__((address_space(4))) rmr_op COp;
+typedef const __attribute__((address_space(4))) float CFloat;
+typedef const __attribute__((address_space(4))) rmr_material CMat;
+typedef const __attribute__((address_space(4))) DPrim CDPrim;
+
+#define PI_F 3.14159274101257324219f
+
+enum Phase : int {
+    PH_IDLE = 0,
+    PH_MARCH = 1,   // march() step of the primary / bounce ray
+    PH_NORMAL = 2,  // getNormal() probe 0..5
+    PH_SHADOW = 3,  // RM2 light-march step
+    PH_HIT = 4,     // march hit, normal ready: run the material
+    PH_MISS = 5,    // march miss: sky
+    PH_NEE = 6,     // RM2: shadow march finished
+    PH_RESTART = 7, // separateChannels: next channel's trace starts at the next refill point
+};
+
+// Per-lane path state. Kept small on purpose (the fast kernels run 8 waves/SIMD = 64 VGPRs):
+//  * the march sign (distMult, RM1:498-505) is `inside`; the march step counter and the
+//    getNormal probe index share `ctr`; getNormal accumulates +probe then subtracts -probe in nrm;
+//  * the primary direction is recomputed from `unit` when separateChannels restarts a trace;
+//  * the sample result goes straight to the sample plane (partial channel sums included);
+//  * HO kernels (hit-in-origin: RM1 without node programs, RM3) keep the hit point in `o`: the
+//    ray origin is dead between a hit and the next bounce there. RM2 (shadow ray from the hit) and
+//    node-program materials (ray.origin is an input of shader_mix / volumeScatter) keep `hit`.
+struct Lane {
+    uint32_t unit;
+    float gxt, gyt, rc;
+    V3 o, d;
+    float t;
+    int ctr;
+    V3 hit;
+    float mid;
+    V3 nrm;
+    V3 color;
+    int chan, bounces;
+    bool inside;
+    float time;    // RM2 samplePDF seed
+    V3 fin;        // RM2 finalColor
+    uint32_t wl;   // RM3 hero wavelength
+    float power;   // RM3
+    int phase;
+};
+template <bool HO> RMR_D V3& hitref(Lane& L) {
+    if constexpr (HO) return L.o;
+    else return L.hit;
+}
+template <bool HO> RMR_D const V3& hitref(const Lane& L) {
+    if constexpr (HO) return L.o;
+    else return L.hit;
+}
+template <int VAR, bool PROG> constexpr bool hit_in_origin() { return VAR != RMR_VARIANT_RM2 && !PROG; }
+
+// ------------------------------------------------------------------------------------------
+// RNG: rand(co), RM1:44-57 (chained fract(sin) hash, state randChange per invocation)
+// ------------------------------------------------------------------------------------------
+RMR_D float rand_step(float gxt, float gyt, float& rc, V2 co) {
+    co.x = fmaf(gxt, rc, co.x);
+    co.y = fmaf(gyt, rc, co.y);
+    float dt = dot2(co, v2(12.9898f, 78.233f));
+    float sn = modf_glsl(dt, 3.14f);
+    rc = fractf(det_sin(sn) * 43758.5453f);
+    return rc;
+}
+RMR_D float lrand(Lane& L, V2 co) { return rand_step(L.gxt, L.gyt, L.rc, co); }
+
+// randHemisphere, RM1:270-304
+RMR_D V3 hemisphere(Lane& L, V2 s1, V2 s2, V3 n) {
+    float theta = 6.28318548202514648438f * lrand(L, s1);
+    float phi = det_acos(2.0f * lrand(L, s2) - 1.0f);
+    float sp, cp, st, ct;
+    det_sincos(phi, sp, cp);
+    det_sincos(theta, st, ct);
+    V3 b = normalize(v3(sp * ct, cp, sp * st));
+    if (!is_zero(n)) {
+        if (b.z < 0.0f) b = -b;
+        V3 lx = veq(n, v3(0.0f, 1.0f, 0.0f)) ? normalize(cross(n, v3(0.0f, 0.0f, 1.0f)))
+                                              : normalize(cross(n, v3(0.0f, 1.0f, 0.0f)));
+        V3 ly = normalize(cross(n, lx));
+        b = mat_mul(lx, ly, n, b);
+    }
+    return b;
+}
+
+// ------------------------------------------------------------------------------------------
+// scene SDF
+// ------------------------------------------------------------------------------------------
+RMR_D float sd_sphere(V3 p, V3 c, float r) { return length(p - c) - r; }            // RM1:170-174
+RMR_D float sd_box(V3 p, V3 c, V3 r) {                                               // RM1:176-180
+    V3 q = vabs(p - c) - r;
+    return fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f) + length(vmax0(q));
+}
+__device__ __noinline__ float sd_mandelbulb(V3 p, V3 c, V3 prm) {
+    V3 p0 = p - c, z = p0;
+    float power = prm.x, bail = prm.z;
+    int iters = (int)prm.y;
+    float dr = 1.0f, r = 0.0f;
+    for (int i = 0; i < iters; i++) {
+        r = length(z);
+        if (r > bail) break;
+        float theta = det_acos(z.z / r);
+        float phi = det_atan2(z.y, z.x);
+        dr = fmaf(det_pow(r, power - 1.0f) * power, dr, 1.0f);
+        float zr = det_pow(r, power);
+        theta = theta * power;
+        phi = phi * power;
+        float st = det_sin(theta);
+        z = vfma(v3(st * det_cos(phi), det_sin(phi) * st, det_cos(theta)), zr, p0);
+    }
+    return 0.5f * det_log(r) * r / dr;
+}
+
+// Register file of a generated function (vec3 vars[total_vars]); indices are wave-uniform.
+struct VarFile {
+    float x[RMR_MAX_VARS], y[RMR_MAX_VARS], z[RMR_MAX_VARS];
+    RMR_D void clear() {
+#pragma unroll
+        for (int i = 0; i < RMR_MAX_VARS; i++) { x[i] = 0.0f; y[i] = 0.0f; z[i] = 0.0f; }
+    }
+    RMR_D V3 get(int i) const { return v3(x[i], y[i], z[i]); }
+    RMR_D void set(int i, V3 v) { x[i] = v.x; y[i] = v.y; z[i] = v.z; }
+};
+
+RMR_D V3 cvec(const KParams& P, int ref) {
+    CFloat* c = (CFloat*)P.consts + 3 * RMR_OPND_CONST_INDEX(ref);
+    return v3(c[0], c[1], c[2]);
+}
+
+// obj_func_j of Graphics.cpp:648-702 — a generic object node program (uniform across the wave)
+__device__ __noinline__ float obj_program(const KParams& P, int begin, int end, int dist_var, V3 p) {
+    VarFile vf;
+    vf.clear();
+    COp* ops = (COp*)P.ops;
+    for (int k = begin; k < end; k++) {
+        int code = ops[k].code;
+        V3 a = v3s(0.0f), b = v3s(0.0f), c = v3s(0.0f), r = v3s(0.0f);
+        int i0 = ops[k].in[0], i1 = ops[k].in[1], i2 = ops[k].in[2];
+        if (i0 != RMR_OPND_NONE) a = (i0 == RMR_OPND_P) ? p : (RMR_OPND_IS_CONST(i0) ? cvec(P, i0) : vf.get(i0));
+        if (i1 != RMR_OPND_NONE) b = (i1 == RMR_OPND_P) ? p : (RMR_OPND_IS_CONST(i1) ? cvec(P, i1) : vf.get(i1));
+        if (i2 != RMR_OPND_NONE) c = (i2 == RMR_OPND_P) ? p : (RMR_OPND_IS_CONST(i2) ? cvec(P, i2) : vf.get(i2));
+        switch (code) {
+        case RMR_OP_GET_X: r = v3s(a.x); break;
+        case RMR_OP_GET_Y: r = v3s(a.y); break;
+        case RMR_OP_GET_Z: r = v3s(a.z); break;
+        case RMR_OP_ADD: r = a + b; break;
+        case RMR_OP_SUB: r = a - b; break;
+        case RMR_OP_MUL: r = a * b; break;
+        case RMR_OP_DIV: r = a / b; break;
+        case RMR_OP_SIN: r = v3(det_sin(a.x), det_sin(a.y), det_sin(a.z)); break;
+        case RMR_OP_COS: r = v3(det_cos(a.x), det_cos(a.y), det_cos(a.z)); break;
+        case RMR_OP_MAP_SPHERE: r = v3s(sd_sphere(a, b, c.x)); break;
+        case RMR_OP_MAP_BOX: r = v3s(sd_box(a, b, c)); break;
+        case RMR_OP_UNION: r = vmin(a, b); break;
+        case RMR_OP_SUBTRACT: r = vmax(a, -b); break;
+        case RMR_OP_INTERSECT: r = vmax(a, b); break;
+        case RMR_OP_DOMAIN_REPEAT:
+            r = a;
+            if (b.x != 0.0f) r.x = modf_glsl(a.x, b.x) - b.x * 0.5f;
+            if (b.y != 0.0f) r.y = modf_glsl(a.y, b.y) - b.y * 0.5f;
+            if (b.z != 0.0f) r.z = modf_glsl(a.z, b.z) - b.z * 0.5f;
+            break;
+        case RMR_OP_MAP_MANDELBULB: r = v3s(sd_mandelbulb(a, b, c)); break;
+        default: break;
+        }
+        vf.set(ops[k].out[0], r);
+    }
+    return vf.get(dist_var).x;
+}
+
+// map(p), RM1:224-231 + the //#OBJINSERT fold (Graphics.cpp:107-112): opU keeps the later object
+// on ties (RM1:219-222). The prim index is wave-uniform: every table read is a scalar load.
+//
+// NP > 0 : sphere/box scene padded to NP prims, loop fully unrolled -> all s_loads issue at the
+//          top of map() and one wait covers them;
+// NP == 0: sphere/box scene of any size, software-pipelined scalar loads (prim j+1 in flight
+//          while prim j is evaluated);
+// NP < 0 : general scene (node programs, Mandelbulb) through the 48-byte rmr_prim rows.
+// opU(a, b) = a.x < b.x ? a : b with the reference's NaN behaviour as compiled by Mesa llvmpipe
+// (per component: distance = min ignoring NaN, id = ordered select; oracle/rmr_oracle.c o_map).
+// Same bits as the plain select for every non-NaN input; d.x never becomes NaN.
+RMR_D void opu(V2& d, float dj, float mid) {
+    const bool take_id = !(d.x < dj);
+    const bool take_d = d.x >= dj;
+    d.y = take_id ? mid : d.y;
+    d.x = take_d ? dj : d.x;
+}
+
+// One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
+// in flight while prim j is evaluated (A/B: +2% over loading at use). The IEEE sqrt sequence hipcc
+// is replaced by rmr::sqrt_cr (same bits, 6 fewer VALU per sqrt; rmr_math.h).
+typedef int int8v __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) int8v CInt8v;
+
+template <int NP>
+RMR_D V2 map_fixed(const KParams& P, V3 p) {
+#ifdef RMR_EXP_CORNELL  // experiment: scenes/cornell5.scene baked in as literals (JIT estimate)
+    V2 d = v2(P.max_dist, -1.0f);
+    opu(d, sd_box(p, v3(0.0f, -1.025f, 0.0f), v3(4.0f, 0.05f, 4.0f)), 0.0f);
+    opu(d, sd_box(p, v3(-3.0f, 1.0f, 0.0f), v3(0.05f, 3.0f, 4.0f)), 1.0f);
+    opu(d, sd_box(p, v3(3.0f, 1.0f, 0.0f), v3(0.05f, 3.0f, 4.0f)), 2.0f);
+    opu(d, sd_sphere(p, v3(0.0f, 0.0f, 0.0f), 1.0f), 0.0f);
+    opu(d, sd_box(p, v3(0.0f, 4.0f, 0.0f), v3(1.5f, 0.05f, 1.5f)), 3.0f);
+    return d;
+#else
+    CInt8v* pr = (CInt8v*)P.dprims;
+    V2 d = v2(P.max_dist, -1.0f);
+    int8v cur = pr[0];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        int8v nxt;
+        if (j + 1 < NP) nxt = pr[j + 1];
+        const int type = cur[6];
+        const V3 c = v3(__int_as_float(cur[0]), __int_as_float(cur[1]), __int_as_float(cur[2]));
+        const V3 r = v3(__int_as_float(cur[3]), __int_as_float(cur[4]), __int_as_float(cur[5]));
+        const float mid = __int_as_float(cur[7]);
+        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
+        if (j + 1 < NP) cur = nxt;
+    }
+    return d;
+#endif
+}
+
+RMR_D V2 map_loop(const KParams& P, V3 p) {
+    CDPrim* pr = (CDPrim*)P.dprims;
+    V2 d = v2(P.max_dist, -1.0f);
+    const int n = P.n_prims;
+    int type = pr[0].type;
+    V3 c = v3(pr[0].c[0], pr[0].c[1], pr[0].c[2]);
+    V3 r = v3(pr[0].r[0], pr[0].r[1], pr[0].r[2]);
+    float mid = pr[0].mat_id;
+    for (int j = 0; j < n; ++j) {
+        const int jn = (j + 1 < n) ? j + 1 : j;
+        const int ntype = pr[jn].type;
+        const V3 nc = v3(pr[jn].c[0], pr[jn].c[1], pr[jn].c[2]);
+        const V3 nr = v3(pr[jn].r[0], pr[jn].r[1], pr[jn].r[2]);
+        const float nmid = pr[jn].mat_id;
+        if (type == RMR_PRIM_BOX) opu(d, sd_box(p, c, r), mid);
+        else if (type == RMR_PRIM_SPHERE) opu(d, sd_sphere(p, c, r.x), mid);
+        type = ntype; c = nc; r = nr; mid = nmid;
+    }
+    return d;
+}
+
+RMR_D V2 map_general(const KParams& P, V3 p) {
+    CPrim* pr = (CPrim*)P.prims;
+    V2 d = v2(P.max_dist, -1.0f);
+    const int n = P.n_prims;
+    for (int j = 0; j < n; ++j) {
+        const int type = pr[j].type;
+        const V3 c = v3(pr[j].c[0], pr[j].c[1], pr[j].c[2]);
+        const V3 r = v3(pr[j].r[0], pr[j].r[1], pr[j].r[2]);
+        float dj;
+        if (type == RMR_PRIM_BOX) dj = sd_box(p, c, r);
+        else if (type == RMR_PRIM_SPHERE) dj = sd_sphere(p, c, r.x);
+        else if (type == RMR_PRIM_MANDELBULB) dj = sd_mandelbulb(p, c, r);
+        else dj = obj_program(P, pr[j].prog_begin, pr[j].prog_end, pr[j].dist_var, p);
+        opu(d, dj, pr[j].mat_id);
+    }
+    return d;
+}
+
+// map() policies of the trace kernel: table-driven (ahead of time, NP as above) or generated per
+// scene (rmr_jit.cpp: struct JitMap with the same eval signature).
+template <int NP>
+struct TableMap {
+    static RMR_D V2 eval(const KParams& P, V3 p) {
+        if constexpr (NP > 0) return map_fixed<NP>(P, p);
+        else if constexpr (NP == 0) return map_loop(P, p);
+        else return map_general(P, p);
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// path bookkeeping shared by the variants
+// ------------------------------------------------------------------------------------------
+RMR_D V3 channel_vec(int chan) {
+    return chan < 0 ? v3s(1.0f) : v3(chan == 0 ? 1.0f : 0.0f, chan == 1 ? 1.0f : 0.0f, chan == 2 ? 1.0f : 0.0f);
+}
+// grayscale, RM1:306-309
+RMR_D float gray_ch(V3 c, int chan) {
+    V3 ch = channel_vec(chan);
+    return (c.x + c.y + c.z) / (ch.x + ch.y + ch.z);
+}
+
+#define PH_DONE (-1)
+
+template <bool HO>
+RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
+    L.t = 0.0f;
+    L.ctr = 0;
+    if (P.max_steps > 0) {
+        L.phase = phase_on_run;
+    } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
+        L.t = P.max_dist;
+        L.phase = PH_NEE;
+    } else {
+        L.t = P.max_dist;
+        L.mid = -1.0f;
+        hitref<HO>(L) = vfma(L.d, L.t, L.o);
+        L.phase = PH_MISS;
+    }
+}
+
+// trace() prologue: o = eye, d = dir, per-variant throughput init (RM1:485-492, RM2:422-429,
+// RM3:349-355). Returns false if the trace has zero bounces (loop body never runs).
+template <int VAR, bool HO>
+RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir) {
+    L.o = v3(P.eye[0], P.eye[1], P.eye[2]);
+    L.d = dir;
+    L.bounces = 0;
+    L.inside = false;
+    if (VAR == RMR_VARIANT_RM1) L.color = channel_vec(L.chan);
+    if (VAR == RMR_VARIANT_RM2) { L.color = v3s(1.0f); L.fin = v3s(0.0f); }
+    if (VAR == RMR_VARIANT_RM3) { L.wl = 0u; L.power = 1.0f; }
+    if (L.bounces < P.max_bounces) {
+        L.bounces = 1;
+        start_march<HO>(P, L, PH_MARCH);
+        return true;
+    }
+    return false;
+}
+
+// unit -> (sample k, pixel); false if the pixel is outside the clip rect
+RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& time) {
+    const uint32_t per_k = (uint32_t)P.n_tiles * 64u;
+    const uint32_t k = u / per_k;
+    const uint32_t rem = u - k * per_k;
+    const int tile = (int)(rem >> 6), lane = (int)(rem & 63u);
+    const TileXY txy = P.tiles[tile];
+    px = txy.x + (lane & 7);
+    py = txy.y + (lane >> 3);
+    time = P.times[k];
+    return !(px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1);
+}
+
+// main(): jittered corner ray, RM1:569-584 (identical in RM2/RM3). The three rand() calls start
+// the invocation's chain (randChange = 0); `rc` returns the chain state after them.
+RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
+    const float gxt = (float)px + time, gyt = (float)py + time;
+    rc = 0.0f;
+    const float W = (float)P.W, H = (float)P.H;
+    const float posx = (float)px / W, posy = (float)py / H;
+    const float j1 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
+    const float j2 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
+    const float j3 = rand_step(gxt, gyt, rc, v2((float)py + time, (float)px + time));
+    const V3 r00 = v3(P.r00[0], P.r00[1], P.r00[2]), r01 = v3(P.r01[0], P.r01[1], P.r01[2]);
+    const V3 r10 = v3(P.r10[0], P.r10[1], P.r10[2]), r11 = v3(P.r11[0], P.r11[1], P.r11[2]);
+    const V3 top = vmix(r00, r01, posx + j1 / W);
+    const V3 bot = vmix(r10, r11, posx + j2 / W);
+    return normalize(vmix(top, bot, posy + j3 / H));
+}
+
+// End of trace(): store the channel result into the sample plane. Returns true when the sample
+// is complete; otherwise (separateChannels, RM1:586-598) the lane is parked in PH_RESTART and the
+// next channel's trace starts where new units start (one inlined copy of the ray setup).
+template <int VAR, bool HO>
+RMR_D bool finish_trace(const KParams& P, Lane& L) {
+    {
+        V3 res;
+        if (VAR == RMR_VARIANT_RM1) res = L.color;
+        if (VAR == RMR_VARIANT_RM2) {
+            if (L.bounces != P.max_bounces) L.fin = L.fin + L.color;   // RM2:514-517
+            res = L.fin;
+        }
+        if (VAR == RMR_VARIANT_RM3) {
+            // wavelengthToColor(range) * power, RM3:447-522 / 540
+            float wl = (float)L.wl, R, G, B, alpha;
+            if (wl >= 380.0f && wl < 440.0f) { R = (-1.0f * (wl - 440.0f)) / 60.0f; G = 0.0f; B = 1.0f; }
+            else if (wl >= 440.0f && wl < 490.0f) { R = 0.0f; G = (wl - 440.0f) / 50.0f; B = 1.0f; }
+            else if (wl >= 490.0f && wl < 510.0f) { R = 0.0f; G = 1.0f; B = (-1.0f * (wl - 510.0f)) / 20.0f; }
+            else if (wl >= 510.0f && wl < 580.0f) { R = (wl - 510.0f) / 70.0f; G = 1.0f; B = 0.0f; }
+            else if (wl >= 580.0f && wl < 645.0f) { R = 1.0f; G = (-1.0f * (wl - 645.0f)) / 65.0f; B = 0.0f; }
+            else if (wl >= 645.0f && wl <= 780.0f) { R = 1.0f; G = 0.0f; B = 0.0f; }
+            else { R = 0.0f; G = 0.0f; B = 0.0f; }
+            if (wl > 780.0f || wl < 380.0f) alpha = 0.0f;
+            else if (wl > 700.0f) alpha = (780.0f - wl) / 80.0f;
+            else if (wl < 420.0f) alpha = (wl - 380.0f) / 40.0f;
+            else alpha = 1.0f;
+            const V3 c = (v3(R, G, B) * alpha) * L.power;
+            P.samp[L.unit] = make_float4(c.x, c.y, c.z, 1.0f);
+            return true;
+        }
+        if (L.chan < 0) {
+            P.samp[L.unit] = make_float4(res.x, res.y, res.z, 1.0f);
+            return true;
+        }
+        // separateChannels: (r + g) + b, RM1:597; the partial sum lives in the sample plane
+        V3 acc = res;
+        if (L.chan != 0) {
+            const float4 pv = P.samp[L.unit];
+            acc = v3(pv.x, pv.y, pv.z) + res;
+        }
+        P.samp[L.unit] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        if (L.chan == 2) return true;
+        L.chan++;
+        L.phase = PH_RESTART;
+        return false;
+    }
+}
+
+// `while (bounces < maxBounces) { bounces++; v = march(o, d, ...) ...}`: next march or trace end
+template <int VAR, bool HO>
+RMR_D void next_bounce(const KParams& P, Lane& L) {
+    if (L.bounces < P.max_bounces) {
+        L.bounces++;
+        start_march<HO>(P, L, PH_MARCH);   // march sign = inside ? -1 : 1
+    } else if (finish_trace<VAR, HO>(P, L)) {
+        L.phase = PH_DONE;
+    }
+}
+
+// main(): jittered corner ray, RM1:569-584 (identical in RM2/RM3)
+// (Re)start a trace: a fresh unit (fresh = true: pixel, seed chain, channel) or the next
+// separateChannels pass of this lane's unit (same primary ray; the rand chain continues).
+template <int VAR, bool HO>
+RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
+    int px, py;
+    float time, rc;
+    const bool in_rect = unit_pixel(P, u, px, py, time);
+    if (fresh && !in_rect) {
+        L.phase = PH_IDLE;
+        return;
+    }
+    const V3 dir = primary_dir(P, px, py, time, rc);
+    if (fresh) {
+        L.unit = u;
+        L.time = time;
+        L.gxt = (float)px + time;
+        L.gyt = (float)py + time;
+        L.rc = rc;
+        L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
+    }
+    for (;;) {  // a zero-bounce trace finishes at once (and may start the next channel)
+        if (trace_prologue<VAR, HO>(P, L, dir)) return;
+        if (finish_trace<VAR, HO>(P, L)) {
+            L.phase = PH_DONE;
+            return;
+        }
+    }
+}
+
+// one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
+// distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
+template <bool HO>
+RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
+    const bool shadow = (L.phase == PH_SHADOW);
+    const float dist = (L.inside && !shadow) ? -m.x : m.x;
+    if (dist < 0.001f) {
+        if (shadow) {          // sd = t; keep hit/mid/normal of the shaded point
+            L.phase = PH_NEE;
+        } else {
+            L.mid = m.y;
+            hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            L.ctr = 0;
+            L.phase = PH_NORMAL;
+        }
+        return;
+    }
+    bool miss = L.t >= P.max_dist;
+    if (!miss) {
+        L.t = fmaf(dist, P.step_mult, L.t);
+        L.ctr++;
+        miss = (L.ctr >= P.max_steps);
+    }
+    if (miss) {
+        L.t = P.max_dist;
+        if (shadow) {
+            L.phase = PH_NEE;
+        } else {
+            L.mid = -1.0f;
+            hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            L.phase = PH_MISS;
+        }
+    }
+}
+
+// getNormal probe order: +x, -x, +y, -y, +z, -z (RM1:263-265).
+// +probes add (+h, +0, +0); -probes add (-h, -0, -0): x + (-0) == x - 0 bit for bit, so this is
+// exactly the oracle's p +- vec3(h,0,0) without a divergent switch (A/B: +10% vs a switch).
+template <bool HO>
+RMR_D V3 probe_point(const Lane& L) {
+    const float h = 0.001f;
+    const int ax = L.ctr >> 1;
+    const bool neg = (L.ctr & 1) != 0;
+    const float hs = neg ? -h : h, z0 = neg ? -0.0f : 0.0f;
+    const V3 hp = hitref<HO>(L);
+    return v3(hp.x + (ax == 0 ? hs : z0), hp.y + (ax == 1 ? hs : z0), hp.z + (ax == 2 ? hs : z0));
+}
+// nrm.c holds map(p + h e_c) after the + probe and map(p + h e_c) - map(p - h e_c) after the - probe
+RMR_D void normal_update(Lane& L, float m) {
+    const int ax = L.ctr >> 1;
+    const bool plus = (L.ctr & 1) == 0;
+    // (no select between struct fields here: clang turns that into a dynamic stack index)
+    const float vx = plus ? m : L.nrm.x - m, vy = plus ? m : L.nrm.y - m, vz = plus ? m : L.nrm.z - m;
+    L.nrm.x = ax == 0 ? vx : L.nrm.x;
+    L.nrm.y = ax == 1 ? vy : L.nrm.y;
+    L.nrm.z = ax == 2 ? vz : L.nrm.z;
+    L.ctr++;
+    if (L.ctr == 6) {
+        L.nrm = normalize(L.nrm);
+        L.phase = PH_HIT;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// RM1 materials: mat_func_j bodies generated by Graphics.cpp:515-645 from v1 node lists
+// ------------------------------------------------------------------------------------------
+RMR_D V3 mat_opnd(const KParams& P, const VarFile& vf, int ref) {
+    if (RMR_OPND_IS_CONST(ref)) return cvec(P, ref);
+    if (ref >= 0) return vf.get(ref);
+    return v3s(0.0f);
+}
+
+// runs material `m` (wave-uniform) for this lane; ray = (o, d, t, hit, inside)
+RMR_D void run_material_v1(const KParams& P, Lane& L, int m, V3& oc, V3& od, V3& oi, V3& oh) {
+    CMat* mats = (CMat*)P.mats;
+    COp* ops = (COp*)P.ops;
+    VarFile vf;
+    vf.clear();
+    const V3 N = L.nrm;
+    const V3 ch = channel_vec(L.chan);
+    const int begin = mats[m].prog_begin, end = mats[m].prog_end;
+    for (int k = begin; k < end; k++) {
+        const int code = ops[k].code;
+        V3 in[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int ref = ops[k].in[i];
+            in[i] = (ref == RMR_OPND_NONE) ? v3s(0.0f) : mat_opnd(P, vf, ref);
+        }
+        V3 o0 = v3s(0.0f), o1 = v3s(0.0f), o2 = v3s(0.0f), o3 = v3s(0.0f);
+        switch (code) {
+        case RMR_OP_M_FACING: {  // RM1:314-317
+            const float sg = (float)((int)L.inside * 2 - 1);
+            o0 = v3s(clampf(dot(L.d * sg, N), 0.0f, 1.0f));
+            break;
+        }
+        case RMR_OP_M_INSIDE: o0 = v3s((float)(int)L.inside); break;
+        case RMR_OP_M_ADD: o0 = in[0] + in[1]; break;
+        case RMR_OP_M_SUB: o0 = in[0] - in[1]; break;
+        case RMR_OP_M_MUL: o0 = in[0] * in[1]; break;
+        case RMR_OP_M_DIV: o0 = in[0] / in[1]; break;
+        case RMR_OP_M_MIX: {  // RM1:346-376
+            const float r = lrand(L, v2(L.o.z, L.o.x));
+            const float f = clampf(gray_ch(in[6] * ch, L.chan), 0.0f, 1.0f);
+            bool second = r < f;
+            if (f == 0.0f) second = false;
+            else if (f == 1.0f) second = true;
+            o0 = second ? in[3] : in[0];
+            o1 = second ? in[4] : in[1];
+            o2 = second ? in[5] : in[2];
+            break;
+        }
+        case RMR_OP_M_DIFFUSE:  // RM1:378-387
+            o0 = in[0];
+            o1 = hemisphere(L, v2(L.hit.x, L.hit.y), v2(L.hit.z, L.hit.x), N);
+            break;
+        case RMR_OP_M_GLOSSY: {  // RM1:389-398
+            o0 = in[0];
+            const V3 hd = hemisphere(L, v2(L.hit.y, L.hit.x), v2(L.hit.x, L.hit.z), N);
+            const float sg = -(float)((int)L.inside * 2 - 1);
+            const V3 rf = reflect(L.d, N * sg);
+            o1 = vmix(hd, rf, 1.0f - gray_ch(in[1] * ch, L.chan));
+            break;
+        }
+        case RMR_OP_M_REFRACTION:  // RM1:400-427
+            o0 = L.inside ? in[0] : v3s(1.0f);
+            if (!L.inside) {
+                o1 = normalize(refract(L.d, N, 1.0f / gray_ch(in[1] * ch, L.chan)));
+                o2 = v3s(1.0f);
+            } else {
+                const V3 rdir = normalize(refract(L.d, -N, gray_ch(in[1] * ch, L.chan)));
+                const V3 ddir = hemisphere(L, v2(L.hit.z, L.hit.y), v2(L.hit.y, L.hit.z), N);
+                o1 = vmix(ddir, rdir, 1.0f - gray_ch(in[2] * ch, L.chan));
+                o2 = v3s(0.0f);
+            }
+            break;
+        case RMR_OP_M_VOLUME:  // RM1:429-474
+            if (L.inside) {
+                const float t = L.t;
+                const float den = gray_ch(in[1] * ch, L.chan) / 20.0f;
+                const int npts = (int)floorf(t * 100.0f);
+                V3 hp = v3s(0.0f);
+                for (int i = 0; i < npts; i++) {
+                    float r = lrand(L, v2(L.hit.x, L.hit.y));
+                    if (r < den) {
+                        r = lrand(L, v2(L.hit.z, L.hit.y)) * t;
+                        hp = vfma(L.d, r, L.o);
+                        break;
+                    }
+                }
+                if (!is_zero(hp)) {
+                    o0 = in[0];
+                    o1 = hemisphere(L, v2(hp.x, hp.y), v2(hp.z, hp.y), v3s(0.0f));
+                    o2 = v3s(1.0f);
+                    o3 = hp;
+                } else {
+                    o0 = v3s(1.0f); o1 = L.d; o2 = v3s(0.0f); o3 = v3s(0.0f);
+                }
+            } else {
+                o0 = v3s(1.0f); o1 = L.d; o2 = v3s(1.0f); o3 = v3s(0.0f);
+            }
+            break;
+        case RMR_OP_M_EMISSION:  // RM1:476-479
+            o0 = in[0] * gray_ch(in[1] * ch, L.chan);
+            break;
+        default: break;
+        }
+        const int w0 = ops[k].out[0], w1 = ops[k].out[1], w2 = ops[k].out[2], w3 = ops[k].out[3];
+        if (w0 >= 0) vf.set(w0, o0);
+        if (w1 >= 0) vf.set(w1, o1);
+        if (w2 >= 0) vf.set(w2, o2);
+        if (w3 >= 0) vf.set(w3, o3);
+    }
+    const int cv = mats[m].color_var, dv = mats[m].dir_var, iv = mats[m].inside_var, hv = mats[m].hit_var;
+    if (cv >= 0) oc = vf.get(cv);
+    if (dv >= 0) od = vf.get(dv);
+    if (iv >= 0) oi = vf.get(iv);
+    if (hv >= 0) oh = vf.get(hv);
+}
+
+// trace() hit tail, RM1:526-553
+template <bool HO>
+RMR_D void rm1_after_material(const KParams& P, Lane& L, V3 nc, V3 nd, V3 ni, V3 nh) {
+    L.color = L.color * nc;
+    L.inside = ni.x != 0.0f;
+    if (is_zero(nd)) {
+        if (finish_trace<RMR_VARIANT_RM1, HO>(P, L)) L.phase = PH_DONE;
+        return;
+    }
+    const V3 hit = hitref<HO>(L);
+    L.d = nd;
+    if (is_zero(nh)) L.o = L.inside ? vfma(L.nrm, -0.002f, hit) : vfma(L.nrm, 0.003f, hit);
+    else L.o = nh;
+    next_bounce<RMR_VARIANT_RM1, HO>(P, L);
+}
+
+// ------------------------------------------------------------------------------------------
+// RM2: NEE + v2 node material
+// ------------------------------------------------------------------------------------------
+RMR_D void make_tbn(V3 N, V3& c0, V3& c1, V3& c2) {  // makeTBN, RM2:211-229
+    const V3 tangent = (N.x == 0.0f) ? v3(1.0f, 0.0f, 0.0f) : normalize(cross(v3(0.0f, 1.0f, 0.0f), N));
+    c0 = normalize(cross(tangent, N));
+    c1 = N;
+    c2 = tangent;
+}
+RMR_D V3 diffuse_sample(Lane& L) {  // material_diffuse.samplePDF, RM2:279-290
+    const float sin2 = lrand(L, v2(L.time, L.time));
+    const float cos2 = 1.0f - sin2;
+    const float st = sqrt_cr(sin2), ct = sqrt_cr(cos2);
+    const float o = (lrand(L, v2(L.time, L.time)) * 2.0f) * PI_F;
+    float so, co;
+    det_sincos(o, so, co);
+    return normalize(v3(st * co, ct, st * so));
+}
+RMR_D V3 glossy_sample(Lane& L, V3 wo, V3 n, float rough) {  // material_glossy.samplePDF, RM2:326-342
+    if (rough == 0.0f) return reflect(wo, n);
+    const float o = (lrand(L, v2(L.time, L.time)) * 2.0f) * PI_F;
+    const float a = pow2(rough);
+    const float r = lrand(L, v2(L.time, L.time));
+    const float th = det_acos(sqrt_cr((1.0f - r) / ((a * a - 1.0f) * r + 1.0f)));
+    float sth, cth, so, co;
+    det_sincos(th, sth, cth);
+    det_sincos(o, so, co);
+    return normalize(v3(sth * co, cth, sth * so));
+}
+// generated mat_func_<id>, Graphics.cpp:705-739 + compileNode 412-463 (program is wave-uniform)
+RMR_D void run_material_v2(const KParams& P, Lane& L, V3 pos, V3 pdir, V3 N, V3 t0, V3 t1, V3 t2,
+                           V3& mat_color, V3& new_dir, bool& will_break) {
+    COp* ops = (COp*)P.ops;
+    VarFile vf;
+    vf.clear();
+    for (int k = P.v2_begin; k < P.v2_end; k++) {
+        const int code = ops[k].code;
+        if (code == RMR_OP_V2_DIFFUSE) {
+            vf.set(ops[k].out[0], mat_mul(t0, t1, t2, diffuse_sample(L)));
+            vf.set(ops[k].out[1], cvec(P, ops[k].in[0]));
+        } else if (code == RMR_OP_V2_GLOSSY) {
+            const float rough = cvec(P, ops[k].in[1]).x;
+            vf.set(ops[k].out[0], mat_mul(t0, t1, t2, glossy_sample(L, pdir, N, rough)));
+            vf.set(ops[k].out[1], cvec(P, ops[k].in[0]));
+        } else if (code == RMR_OP_V2_FRESNEL) {
+            vf.set(ops[k].out[0], v3s(pow5(1.0f - clampf(dot(N, pdir), 0.0f, 1.0f)) * 0.96f + 0.04f));
+        } else if (code == RMR_OP_V2_MIX) {
+            const float r = lrand(L, v2(pos.x, pos.z));
+            const bool second = r <= vf.get(ops[k].in[4]).x;
+            const V3 dsel = second ? vf.get(ops[k].in[2]) : vf.get(ops[k].in[0]);
+            const V3 rsel = second ? vf.get(ops[k].in[3]) : vf.get(ops[k].in[1]);
+            vf.set(ops[k].out[0], dsel);
+            vf.set(ops[k].out[1], rsel);
+        }
+    }
+    const V3 refl = vf.get(1);
+    new_dir = vf.get(0);
+    const float prob = fmaxf(refl.x, fmaxf(refl.y, refl.z));
+    mat_color = L.color;
+    if (lrand(L, v2(pos.z, pos.x)) <= 1.0f) {
+        mat_color = mat_color * (refl / v3s(prob));
+        will_break = false;
+    } else {
+        will_break = true;
+    }
+}
+RMR_D V3 rm2_albedo(const KParams& P, int id) {
+    if (id < 0 || id >= RMR_MAX_MATERIALS) return v3s(0.0f);
+    const float* a = P.rm2->albedo[id];
+    return v3(a[0], a[1], a[2]);
+}
+
+// ------------------------------------------------------------------------------------------
+// RM3: spectral event (mat_func_k RM3:251-345, sky RM3:408-438)
+// ------------------------------------------------------------------------------------------
+RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) {
+    if (L.wl == 0u) {
+        float r = lrand(L, seed);
+        r = r * (float)((mx - mn) / 5u);
+        r = floorf(r) * 5.0f;
+        L.wl = (uint32_t)(int)r + mn;
+        L.power = L.power * pw;
+        return false;
+    }
+    if (L.wl < mn || L.wl > mx) { L.wl = 0u; return true; }
+    L.power = L.power * pw;
+    return false;
+}
+
+// ------------------------------------------------------------------------------------------
+// shading of the parked lanes
+// ------------------------------------------------------------------------------------------
+template <int VAR, bool PROG>
+RMR_D void shade(const KParams& P, Lane& L) {
+    constexpr bool HO = hit_in_origin<VAR, PROG>();
+    if (VAR == RMR_VARIANT_RM1) {
+        const bool want = (L.phase == PH_HIT);
+        const int id = want ? (int)L.mid : -1;
+        int kind = MAT_NONE;
+        DMat dm;
+        if (want && id >= 0 && id < P.n_mats) {
+            dm = P.dmats[id];
+            kind = dm.kind;
+        }
+        V3 nc = v3s(0.0f), nd = v3s(0.0f), ni = v3s(0.0f), nh = v3s(0.0f);
+        if (kind == MAT_DIFFUSE) {          // shader_diffuse(ray, c, color, dir), RM1:378-387
+            nc = v3(dm.c[0], dm.c[1], dm.c[2]);
+            const V3 hp = hitref<HO>(L);
+            nd = hemisphere(L, v2(hp.x, hp.y), v2(hp.z, hp.x), L.nrm);
+        } else if (kind == MAT_EMISSION) {  // shader_emission(ray, c, p, color), RM1:476-479
+            nc = v3(dm.c[0], dm.c[1], dm.c[2]) * gray_ch(v3(dm.p[0], dm.p[1], dm.p[2]) * channel_vec(L.chan), L.chan);
+        }
+        if constexpr (PROG) {  // generic node programs, one wave-uniform material at a time
+            const bool valid = (kind == MAT_PROGRAM);
+            uint64_t pending = __ballot(valid);
+            while (pending) {
+                const int lead = __ffsll((unsigned long long)pending) - 1;
+                const int m = __builtin_amdgcn_readlane(id, lead);
+                const bool mine = valid && id == m;
+                if (mine) run_material_v1(P, L, m, nc, nd, ni, nh);
+                pending &= ~__ballot(mine);
+            }
+        }
+        if (want) rm1_after_material<HO>(P, L, nc, nd, ni, nh);
+        if (L.phase == PH_MISS) {  // shader_emission(ray, skyColor(dir), vec3(1), emit), RM1:555-561
+            const V3 emit = v3(P.sky[0], P.sky[1], P.sky[2]) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
+            L.color = L.color * emit;
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+        }
+    }
+    if (VAR == RMR_VARIANT_RM2) {
+        const V3 lp = v3(P.rm2_light[0], P.rm2_light[1], P.rm2_light[2]);
+        if (L.phase == PH_HIT) {  // RM2:436-506
+            const V3 pos = hitref<HO>(L), N = L.nrm, pdir = -L.d;
+            const int id = (int)L.mid;
+            if (id == P.rm2_node_id) {
+                V3 t0, t1, t2;
+                make_tbn(N, t0, t1, t2);
+                V3 matc, nd;
+                bool wb;
+                run_material_v2(P, L, pos, pdir, N, t0, t1, t2, matc, nd, wb);
+                L.color = L.color * matc;
+                if (wb) {
+                    L.color = v3s(0.0f);
+                    if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+                } else {
+                    L.o = vfma(N, 0.002f, pos);
+                    L.d = nd;
+                    next_bounce<VAR, HO>(P, L);
+                }
+            } else {  // light-march toward the point light, RM2:481
+                L.o = vfma(N, 0.002f, pos);
+                L.d = normalize(lp - pos);
+                start_march<HO>(P, L, PH_SHADOW);   // hit/mid/nrm stay for the NEE step
+            }
+        } else if (L.phase == PH_NEE) {  // RM2:482-501
+            const V3 pos = hitref<HO>(L), N = L.nrm;
+            const float sd = L.t;
+            const V3 mc = rm2_albedo(P, (int)L.mid);
+            const V3 ld = normalize(lp - pos);
+            const float len = length(lp - pos);
+            if (sd >= len) {
+                const V3 brdf = v3(mc.x / PI_F, mc.y / PI_F, mc.z / PI_F);
+                V3 c = L.color * brdf;
+                c = c * clampf(dot(ld, N), 0.0f, 1.0f);
+                c = c * (P.rm2_light_power / pow2(len));
+                L.fin = L.fin + c;
+            }
+            V3 t0, t1, t2;
+            make_tbn(N, t0, t1, t2);
+            const V3 nd = mat_mul(t0, t1, t2, diffuse_sample(L));
+            const float prob = fmaxf(mc.x, fmaxf(mc.y, mc.z));
+            if (lrand(L, v2(pos.z, pos.x)) <= prob) {
+                L.color = L.color * (mc / v3s(prob));
+                L.o = vfma(N, 0.002f, pos);
+                L.d = nd;
+                next_bounce<VAR, HO>(P, L);
+            } else {
+                L.color = v3s(0.0f);
+                if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+            }
+        } else if (L.phase == PH_MISS) {
+            L.color = L.color * v3(P.sky[0], P.sky[1], P.sky[2]);
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+        }
+    }
+    if (VAR == RMR_VARIANT_RM3) {
+        if (L.phase == PH_HIT) {  // RM3:368-406
+            const V3 pos = hitref<HO>(L), N = L.nrm;
+            const int id = (int)L.mid;
+            V3 nd = v3s(0.0f);
+            bool stop = false;
+            if (id >= 0 && id < P.n_mats && P.spec[id].defined) {
+                const rmr_spectral s = P.spec[id];
+                if (spectral_event(L, s.min_wave, s.max_wave, s.power, v2(pos.y, pos.x))) stop = true;
+                else if (s.terminates) stop = true;
+                else nd = hemisphere(L, v2(pos.x, pos.y), v2(pos.z, pos.y), N);
+            }
+            if (stop) {
+                if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+            } else {
+                L.o = vfma(N, 0.002f, pos);
+                L.d = nd;
+                next_bounce<VAR, HO>(P, L);
+            }
+        } else if (L.phase == PH_MISS) {  // RM3:408-438
+            const V3 pos = hitref<HO>(L);
+            spectral_event(L, P.spec_sky.min_wave, P.spec_sky.max_wave, P.spec_sky.power, v2(pos.y, pos.x));
+            if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
+        }
+    }
+}
+
+RMR_D bool is_active(int ph) { return ph == PH_MARCH || ph == PH_NORMAL || ph == PH_SHADOW; }
+RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_NEE; }
+
+// ------------------------------------------------------------------------------------------
+// the trace kernel
+// ------------------------------------------------------------------------------------------
+// Occupancy target (waves per SIMD) for the fast specialisations: the kernel is latency-bound
+// (scalar-load and dependent-chain stalls), and 8 waves/SIMD measured +8% over the 5 that the
+// register allocator picks unconstrained. The general/interpreter kernels keep their registers.
+#ifndef RMR_FAST_WAVES
+#define RMR_FAST_WAVES 8
+#endif
+// waves/SIMD the register allocator targets (launch bounds of the kernels that call trace_main)
+template <int VAR, bool GENERAL, bool PROG>
+constexpr int trace_waves() { return (GENERAL || PROG || VAR == RMR_VARIANT_RM2) ? 1 : RMR_FAST_WAVES; }
+
+template <int VAR, class MAP, bool PERSIST, bool PROG>
+RMR_D void trace_main(const KParams& P) {
+    constexpr bool HO = hit_in_origin<VAR, PROG>();
+    Lane L;
+    L.phase = PH_IDLE;
+    uint64_t maps = 0, iters = 0, shades = 0;
+    constexpr uint32_t CHUNK = 128;
+    const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
+    uint32_t rnext = 0, rend = 0;
+    bool exhausted = false;
+    if (!PERSIST) {
+        const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+        if (u < n_units) begin_trace<VAR, HO>(P, L, u, true);
+        exhausted = true;
+    }
+    const int T = P.shade_threshold, TR = P.refill_threshold;
+#ifdef RMR_PROFILE
+    uint64_t cyc[3] = {0, 0, 0};
+    const uint64_t c_begin = __builtin_amdgcn_s_memtime();
+#define RMR_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define RMR_STAMP(v)
+#endif
+    for (;;) {
+        RMR_STAMP(c0);
+        bool fresh = false;
+        uint32_t fu = 0;
+        if (PERSIST && !exhausted) {
+            uint64_t idle = __ballot(L.phase == PH_IDLE);
+            uint64_t act0 = __ballot(is_active(L.phase));
+            if (idle && (__popcll(idle) >= TR || act0 == 0)) {
+                if (rnext >= rend) {
+                    unsigned int base = 0;
+                    if (__lane_id() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK);
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    rnext = base;
+                    exhausted = base >= n_units;
+                    rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
+                }
+                if (!exhausted) {
+                    const uint32_t avail = rend - rnext;
+                    const uint32_t nidle = (uint32_t)__popcll(idle);
+                    const uint32_t take = avail < nidle ? avail : nidle;
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (L.phase == PH_IDLE && rank < take) {
+                        fresh = true;
+                        fu = rnext + rank;
+                    }
+                    rnext += take;
+                }
+            }
+        }
+        const bool restart = (L.phase == PH_RESTART);
+        if (__ballot(fresh || restart)) {
+            if (fresh || restart) begin_trace<VAR, HO>(P, L, fresh ? fu : L.unit, fresh);
+        }
+        RMR_STAMP(c1);
+        const bool act = is_active(L.phase);
+        const uint64_t amask = __ballot(act);
+        if (amask) {
+            if (act) {
+                const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
+                const V2 m = MAP::eval(P, p);
+                if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                else march_update<HO>(P, L, m);
+            }
+            maps += (uint64_t)__popcll(amask);
+            iters++;
+        }
+        RMR_STAMP(c2);
+        const uint64_t smask = __ballot(is_shade(L.phase));
+        const uint64_t amask2 = __ballot(is_active(L.phase));
+        if (smask && (__popcll(smask) >= T || amask2 == 0)) {
+            shades++;
+            if (is_shade(L.phase)) shade<VAR, PROG>(P, L);
+        }
+        // finished samples have stored their radiance (finish_trace): the lane is free
+        if (L.phase == PH_DONE) L.phase = PH_IDLE;
+#ifdef RMR_PROFILE
+        RMR_STAMP(c3);
+        cyc[0] += c1 - c0;
+        cyc[1] += c2 - c1;
+        cyc[2] += c3 - c2;
+#endif
+        const uint64_t live = __ballot(L.phase != PH_IDLE);
+        if (live == 0 && exhausted) break;
+    }
+    if (__lane_id() == 0) {
+        atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
+        atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
+        atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
+#ifdef RMR_PROFILE
+        atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
+        atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);
+        atomicAdd(P.counters + 6, (unsigned long long)cyc[2]);
+        atomicAdd(P.counters + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
+#endif
+    }
+}
+
+// Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
+RMR_D void fold_main(const KParams& P) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int tile = gid >> 6, lane = gid & 63;
+    if (tile >= P.n_tiles) return;
+    const TileXY txy = P.tiles[tile];
+    const int px = txy.x + (lane & 7), py = txy.y + (lane >> 3);
+    if (px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1) return;
+    float4* ap = P.accum + (size_t)py * P.W + px;
+    float4 acc = *ap;
+    const size_t plane = (size_t)P.n_tiles * 64;
+    for (uint32_t k = 0; k < P.nspp; k++) {
+        const float4 c = P.samp[(size_t)k * plane + (size_t)tile * 64 + lane];
+        const uint32_t n = P.first_sample + k;
+        if (n != 0u) {
+            const float f1 = 1.0f / (float)(n + 1u);
+            const float f2 = (float)n / (float)(n + 1u);
+            acc.x = c.x * f1 + acc.x * f2;
+            acc.y = c.y * f1 + acc.y * f2;
+            acc.z = c.z * f1 + acc.z * f2;
+        } else {
+            acc.x = c.x; acc.y = c.y; acc.z = c.z;
+        }
+        acc.w = 1.0f;
+    }
+    *ap = acc;
+}
+
+}  // namespace rmr
+

@@ -153,6 +153,10 @@ class Renderer:
     def set_tuning(self, shade_threshold=0, grid_per_cu=-1, samp_budget=0):
         _check(self._ctx, lib().rmr_set_tuning(self._ctx, int(shade_threshold), int(grid_per_cu), int(samp_budget)))
 
+    def set_jit(self, mode):
+        """hipRTC per-scene kernel specialisation: 0 off, 1 always, 2 auto (large launches)."""
+        _check(self._ctx, lib().rmr_set_jit(self._ctx, int(mode)))
+
     def set_stream(self, hip_stream_handle):
         _check(self._ctx, lib().rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
 
@@ -220,6 +224,26 @@ class Renderer:
 
     def reset_stats(self):
         _check(self._ctx, lib().rmr_reset_stats(self._ctx))
+
+
+def jit_compile_scene(scene, variant):
+    """Compile the hipRTC-specialised trace kernel of a scene (no GPU needed). Returns the
+    code-object key; raises RMRError with the compiler log on failure."""
+    if isinstance(variant, str):
+        variant = abi.VARIANTS[variant]
+    if scene is None:
+        text = b""
+    elif isinstance(scene, dict):
+        text = json.dumps(scene).encode()
+    elif os.path.exists(scene):
+        text = open(scene, "rb").read()
+    else:
+        text = scene.encode()
+    log = C.create_string_buffer(65536)
+    rc = lib().rmr_jit_compile_scene(int(variant), text or None, len(text), log, len(log))
+    if rc != abi.RMR_OK:
+        raise RMRError(rc, log.value.decode(errors="replace"))
+    return log.value.decode()
 
 
 def encode_bmp(rgba, path):

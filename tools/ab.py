@@ -76,6 +76,14 @@ def main():
             L.rmr_get_stats(h, C.byref(st))
             if rnd > 0:
                 res[p].append(st.trace_ms)
+            if rnd == args.rounds and hasattr(L, "rmr_get_section_cycles"):
+                cy = (C.c_uint64 * 4)()
+                L.rmr_get_section_cycles(h, cy)
+                if cy[3]:
+                    print(json.dumps({"lib": os.path.basename(p), "cycles_refill": cy[0] / cy[3],
+                                      "cycles_map": cy[1] / cy[3], "cycles_shade": cy[2] / cy[3],
+                                      "lane_util": st.map_evals / (64.0 * max(1, st.map_iters)),
+                                      "maps_per_iter_batch": st.map_iters / max(1, st.shade_batches)}), flush=True)
             if rnd == args.rounds:
                 a = np.zeros((args.H, args.W, 4), np.float32)
                 L.rmr_read_accum(h, a.ctypes.data_as(C.POINTER(C.c_float)), a.nbytes)

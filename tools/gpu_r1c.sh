@@ -1,0 +1,9 @@
+#!/bin/bash
+cd "$(dirname "$0")/.." || exit 2
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/probes/sqrt_exhaustive > gpurun_out/sqrt_exh.log 2>&1; echo "sqrt rc=$?"; cat gpurun_out/sqrt_exh.log
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py tests/test_host_cpp.py -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python tools/ab.py raymarchrenderer_amd/librmr_plainsqrt.so raymarchrenderer_amd/librmr.so raymarchrenderer_amd/librmr_prof.so --spp 8 --rounds 6 > gpurun_out/ab_r1c.log 2>&1 || exit $?
+cat gpurun_out/ab_r1c.log

@@ -33,7 +33,7 @@ configs = json.loads(args.configs) if args.configs else [
     {"kernel": 0, "T": 24, "grid": 2}, {"kernel": 0, "T": 24, "grid": 8}]
 for cfg in configs:
     r.set_kernel(cfg.get("kernel", 0))
-    r.set_tuning(shade_threshold=cfg.get("T", 24), grid_per_cu=cfg.get("grid", 0))
+    r.set_tuning(shade_threshold=cfg.get("T", 24) | (cfg.get("TR", 0) << 8), grid_per_cu=cfg.get("grid", 0))
     r.render_spp(times[:2])
     r.sync()
     r.reset_stats()
