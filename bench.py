@@ -180,7 +180,8 @@ def main():
                 traffic = None
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "k_trace<RM1,persistent>", "avg_launch_ms": round(per_launch_ms, 3),
+                "kernel": ("rmr_jit_trace (hipRTC scene-specialised trace kernel)" if st.jit_launches
+                           else "k_trace<RM1,persistent>"), "avg_launch_ms": round(per_launch_ms, 3),
                 "map_evals_per_launch": int(st.map_evals / st.trace_launches),
                 "flops_per_map": st.flops_per_map,
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
