@@ -55,6 +55,9 @@ struct rmr_ctx {
     rmr_rm2_consts* d_rm2 = nullptr;
     rmr::DPrim* d_dprims = nullptr;
     rmr::DMat* d_dmats = nullptr;
+    rmr::BvhNode* d_bvh = nullptr;
+    int n_bvh = 0;
+    float bvh_margin = 1e-4f;
     int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
     bool has_prog = true;  // RM1 scene has materials needing the generic node interpreter
     // buffers
@@ -129,6 +132,13 @@ void default_view(rmr_ctx* c) {
     c->view_set = true;
 }
 
+// Scenes of more than kMaxLoopPrims spheres/boxes use the exact-culling BVH map (map_bvh in
+// rmr_trace.h): median-split hierarchy over the primitives' boxes, leaves of <= 4, pre-order with
+// skip links; the primitives are stored in leaf order with their scene index (the id tie-break).
+constexpr size_t kMaxLoopPrims = 32;
+
+int upload_bvh(rmr_ctx* c);
+
 int upload_scene(rmr_ctx* c) {
     const CompiledScene& s = c->scene;
     int r;
@@ -142,19 +152,24 @@ int upload_scene(rmr_ctx* c) {
     bool simple = true;
     for (const auto& p : s.prims) simple = simple && (p.type == RMR_PRIM_SPHERE || p.type == RMR_PRIM_BOX);
     const size_t n = s.prims.size();
-    c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : 0));
-    std::vector<rmr::DPrim> dp(std::max<size_t>(n, 8));
-    for (size_t i = 0; i < dp.size(); i++) {
-        rmr::DPrim q{};
-        if (i < n) {
-            const rmr_prim& p = s.prims[i];
-            for (int k = 0; k < 3; k++) { q.c[k] = p.c[k]; q.r[k] = p.r[k]; }
-            q.type = p.type;
-            q.mat_id = p.mat_id;
+    c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : (n <= kMaxLoopPrims ? 0 : -2)));
+    if (c->map_np == -2) {
+        if ((r = upload_bvh(c))) return r;
+    } else {
+        std::vector<rmr::DPrim> dp(std::max<size_t>(n, 8));
+        for (size_t i = 0; i < dp.size(); i++) {
+            rmr::DPrim q{};
+            if (i < n) {
+                const rmr_prim& p = s.prims[i];
+                for (int k = 0; k < 3; k++) { q.c[k] = p.c[k]; q.r[k] = p.r[k]; }
+                q.type = p.type;
+                q.mat_id = p.mat_id;
+            }
+            dp[i] = q;
         }
-        dp[i] = q;
+        if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
+        c->n_bvh = 0;
     }
-    if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
     // shading kinds (RM1): recognise the single-node diffuse / emission materials
     std::vector<rmr::DMat> dm(std::max<size_t>(1, s.materials.size()));
     for (size_t i = 0; i < s.materials.size(); i++) {
@@ -215,6 +230,104 @@ int ensure_jit(rmr_ctx* c) {
     c->jit_loaded.push_back(k);
     c->jit = k;
     c->jit_ready = true;
+    return RMR_OK;
+}
+
+namespace {
+struct BvhItem {
+    float lo[3], hi[3], cen[3];
+    int idx;
+};
+void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>& nodes, std::vector<int>& order) {
+    const int me = (int)nodes.size();
+    nodes.push_back(rmr::BvhNode{});
+    rmr::BvhNode nd{};
+    for (int k = 0; k < 3; k++) { nd.lo[k] = 3.0e38f; nd.hi[k] = -3.0e38f; }
+    float clo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, chi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+    for (int i = l; i < r; i++)
+        for (int k = 0; k < 3; k++) {
+            nd.lo[k] = std::min(nd.lo[k], it[i].lo[k]);
+            nd.hi[k] = std::max(nd.hi[k], it[i].hi[k]);
+            clo[k] = std::min(clo[k], it[i].cen[k]);
+            chi[k] = std::max(chi[k], it[i].cen[k]);
+        }
+    if (r - l <= 4) {
+        std::sort(it.begin() + l, it.begin() + r, [](const BvhItem& a, const BvhItem& b) { return a.idx < b.idx; });
+        nd.first = (int)order.size();
+        nd.count = r - l;
+        for (int i = l; i < r; i++) order.push_back(it[i].idx);
+    } else {
+        int ax = 0;
+        for (int k = 1; k < 3; k++)
+            if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+        const int mid = (l + r) / 2;
+        std::nth_element(it.begin() + l, it.begin() + mid, it.begin() + r,
+                         [ax](const BvhItem& a, const BvhItem& b) { return a.cen[ax] < b.cen[ax]; });
+        nd.first = -1;
+        nd.count = 0;
+        bvh_build(it, l, mid, nodes, order);
+        bvh_build(it, mid, r, nodes, order);
+    }
+    nd.skip = (int)nodes.size();
+    nodes[(size_t)me] = nd;
+}
+}  // namespace
+
+int upload_bvh(rmr_ctx* c) {
+    const CompiledScene& s = c->scene;
+    std::vector<BvhItem> items;
+    float extent = 0.0f;
+    for (size_t i = 0; i < s.prims.size(); i++) {
+        const rmr_prim& p = s.prims[i];
+        BvhItem b{};
+        for (int k = 0; k < 3; k++) {
+            const float h = (p.type == RMR_PRIM_SPHERE) ? std::fabs(p.r[0]) : std::fabs(p.r[k]);
+            b.lo[k] = p.c[k] - h;
+            b.hi[k] = p.c[k] + h;
+            b.cen[k] = p.c[k];
+            extent = std::max(extent, std::fabs(p.c[k]) + h);
+        }
+        b.idx = (int)i;
+        items.push_back(b);
+    }
+    // Primitives much larger than the typical one (ground planes, walls) would make every box
+    // above them cover the scene: they go first, in an always-visited leaf (infinite bounds), which
+    // also gives the running minimum a small value early.
+    std::vector<float> ext;
+    for (const auto& b : items) ext.push_back(std::max({b.hi[0] - b.lo[0], b.hi[1] - b.lo[1], b.hi[2] - b.lo[2]}));
+    std::vector<float> sorted_ext = ext;
+    std::nth_element(sorted_ext.begin(), sorted_ext.begin() + sorted_ext.size() / 2, sorted_ext.end());
+    const float big = 8.0f * sorted_ext[sorted_ext.size() / 2];
+    std::vector<BvhItem> small, large;
+    for (size_t i = 0; i < items.size(); i++) (ext[i] > big ? large : small).push_back(items[i]);
+    std::vector<rmr::BvhNode> nodes;
+    std::vector<int> order;
+    if (!large.empty()) {
+        for (size_t at = 0; at < large.size(); at += 4) {  // leaves of <= 4, all always visited
+            rmr::BvhNode nd{};
+            for (int k = 0; k < 3; k++) { nd.lo[k] = -3.0e38f; nd.hi[k] = 3.0e38f; }
+            nd.first = (int)order.size();
+            nd.count = (int)std::min<size_t>(4, large.size() - at);
+            for (int i = 0; i < nd.count; i++) order.push_back(large[at + (size_t)i].idx);
+            nd.skip = (int)nodes.size() + 1;
+            nodes.push_back(nd);
+        }
+    }
+    if (!small.empty()) bvh_build(small, 0, (int)small.size(), nodes, order);
+    std::vector<rmr::DPrim> dp(order.size());
+    for (size_t k = 0; k < order.size(); k++) {
+        const rmr_prim& p = s.prims[(size_t)order[k]];
+        rmr::DPrim q{};
+        for (int i = 0; i < 3; i++) { q.c[i] = p.c[i]; q.r[i] = p.r[i]; }
+        q.type = p.type | (order[k] << 8);
+        q.mat_id = p.mat_id;
+        dp[k] = q;
+    }
+    int r;
+    if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
+    if ((r = dev_upload(c, &c->d_bvh, nodes.data(), nodes.size()))) return r;
+    c->n_bvh = (int)nodes.size();
+    c->bvh_margin = 1e-4f + extent * 0x1p-16f;
     return RMR_OK;
 }
 
@@ -327,6 +440,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.prims = c->d_prims; P.ops = c->d_ops; P.consts = c->d_consts; P.mats = c->d_mats;
     P.spec = c->d_spec; P.rm2 = c->d_rm2;
     P.dprims = c->d_dprims; P.dmats = c->d_dmats;
+    P.bvh = c->d_bvh; P.n_nodes = c->n_bvh; P.bvh_margin = c->bvh_margin;
     P.n_prims = (int)s.prims.size();
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
@@ -460,7 +574,7 @@ void rmr_destroy(rmr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
-    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_samp,
+    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_samp,
                     c->d_tiles, c->d_times, c->d_queue, c->d_counters};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

@@ -33,6 +33,19 @@ struct DMat {
     int32_t pad;
 };
 
+// Bounding-volume node of the exact culling map (NP = -2, scenes of more than 32 spheres/boxes).
+// Nodes are in depth-first pre-order: the first child of an internal node is the next node,
+// `skip` is the node after the whole subtree. Leaves hold `count` primitives starting at `first`
+// in the leaf-ordered DPrim array (DPrim.type carries the original scene index in bits 8..31).
+struct BvhNode {
+    float lo[3];
+    int32_t first;
+    float hi[3];
+    int32_t count;   // 0 = internal node
+    int32_t skip;
+    int32_t pad[3];
+};
+
 struct KParams {
     // ---- scene tables (device pointers, read-only) ----
     const rmr_prim* prims;
@@ -43,6 +56,9 @@ struct KParams {
     const rmr_rm2_consts* rm2;
     const DPrim* dprims;        // packed prims (fast map paths)
     const DMat* dmats;          // per-id shading kind (RM1)
+    const BvhNode* bvh;         // NP = -2: node array (n_nodes), prims in dprims in leaf order
+    int32_t n_nodes;
+    float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)
     int32_t n_prims;
     int32_t n_mats;
     int32_t v2_begin, v2_end;

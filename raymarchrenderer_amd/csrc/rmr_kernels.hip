@@ -8,7 +8,7 @@
 namespace rmr {
 
 template <int VAR, int NP, bool PERSIST, bool PROG>
-__global__ __launch_bounds__(256, (trace_waves<VAR, (NP < 0), PROG>())) void k_trace(KParams P) {
+__global__ __launch_bounds__(256, (trace_waves<VAR, (NP == -1), PROG>())) void k_trace(KParams P) {
     trace_main<VAR, TableMap<NP>, PERSIST, PROG>(P);
 }
 
@@ -23,6 +23,7 @@ namespace rmr {
     case 4: CALL(V, 4, PERS, PRG); break;                   \
     case 8: CALL(V, 8, PERS, PRG); break;                   \
     case 0: CALL(V, 0, PERS, PRG); break;                   \
+    case -2: CALL(V, -2, PERS, PRG); break;                 \
     default: CALL(V, -1, PERS, PRG); break;                 \
     }
 #define RMR_LAUNCH(V, NPV, PERS, PRG) k_trace<V, NPV, PERS, PRG><<<g, block, 0, s>>>(P)

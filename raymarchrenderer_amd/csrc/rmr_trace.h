@@ -225,6 +225,29 @@ RMR_D void opu(V2& d, float dj, float mid) {
     d.x = take_d ? dj : d.x;
 }
 
+// Exact culling for the per-scene specialised map() (rmr_jit.cpp). opU's result (distance, id) is
+// unchanged by a primitive whose distance is strictly greater than the running minimum d.x (never
+// NaN), so a wave may skip a primitive when, for every active lane, a lower bound of its distance
+// exceeds d.x + |d.x| 2^-20 + 2^-100. The bounds, in float: box: max(q) (sd_box = min(max q, 0) +
+// sqrt_cr(len2) >= max q up to the last ulp of the sqrt); sphere: sqrt_cr(len2) - r with len2
+// compared against (d.x + r)^2 widened by the same margin. Lanes that evaluate compute exactly the
+// table expressions (sd_box / sd_sphere), so the results stay bit-identical.
+RMR_D float cull_threshold(float dx) { return fmaf(fabsf(dx), 0x1p-20f, dx) + 0x1p-100f; }
+RMR_D void opu_box_culled(V2& d, V3 p, V3 c, V3 r, float mid) {
+    const V3 q = vabs(p - c) - r;
+    const float mq = fmaxf(q.x, fmaxf(q.y, q.z));
+    const bool need = !(mq > cull_threshold(d.x));
+    if (__ballot(need)) opu(d, fminf(mq, 0.0f) + length(vmax0(q)), mid);
+}
+RMR_D void opu_sphere_culled(V2& d, V3 p, V3 c, float r, float mid) {
+    const V3 v = p - c;
+    const float len2 = dot(v, v);
+    const float t = cull_threshold(d.x + r);
+    const bool far = (d.x + r < 0.0f) || (t > 0.0f && len2 > t * t * (1.0f + 0x1p-20f));
+    if (__ballot(!far)) opu(d, sqrt_cr(len2) - r, mid);
+}
+
+
 // One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
 // in flight while prim j is evaluated (A/B: +2% over loading at use). The IEEE sqrt sequence hipcc
 // is replaced by rmr::sqrt_cr (same bits, 6 fewer VALU per sqrt; rmr_math.h).
@@ -302,11 +325,54 @@ RMR_D V2 map_general(const KParams& P, V3 p) {
 
 // map() policies of the trace kernel: table-driven (ahead of time, NP as above) or generated per
 // scene (rmr_jit.cpp: struct JitMap with the same eval signature).
+// NP == -2: exact culling through a bounding-volume hierarchy (scenes of > 32 spheres/boxes).
+// opU's sequential fold (RM1:219-231 with the NaN rule of opu()) has an order-free closed form:
+// distance = min(maxDist, all non-NaN dj); id = the id of the highest scene index j whose dj equals
+// that minimum or is NaN (-1 if none). So primitives may be visited in any order and skipped when
+// they cannot attain the minimum: a node is skipped when, for every active lane, the distance from
+// p to the node's box exceeds the running minimum by a margin (|d| 2^-18 + bvh_margin, the latter
+// 1e-4 + 2^-16 x the scene extent — sd_box/sd_sphere are >= that Euclidean distance up to a few
+// ulps of the coordinates). Traversal is wave-uniform (stackless pre-order
+// with skip links), so node and primitive reads stay scalar loads.
+RMR_D V2 map_bvh(const KParams& P, V3 p) {
+    typedef const __attribute__((address_space(4))) BvhNode CNode;
+    CNode* nodes = (CNode*)P.bvh;
+    CDPrim* pr = (CDPrim*)P.dprims;
+    float dbest = P.max_dist, mbest = -1.0f, mnan = -1.0f;
+    int jbest = -1, jnan = -1;
+    int i = 0;
+    while (i < P.n_nodes) {
+        const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
+        const V3 hi = v3(nodes[i].hi[0], nodes[i].hi[1], nodes[i].hi[2]);
+        const int count = nodes[i].count, skip = nodes[i].skip;
+        const V3 q = vmax0(vmax(lo - p, p - hi));
+        const float lb2 = dot(q, q);
+        const float t = fmaxf(dbest + fmaf(fabsf(dbest), 0x1p-18f, P.bvh_margin), P.bvh_margin);
+        const bool need = !(lb2 > t * t);   // NaN p: lb2 NaN -> needed
+        if (!__ballot(need)) { i = skip; continue; }
+        if (count == 0) { i++; continue; }
+        const int first = nodes[i].first;
+        for (int k = first; k < first + count; k++) {
+            const int tw = pr[k].type;
+            const int type = tw & 0xff, j = tw >> 8;
+            const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
+            const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
+            const float mid = pr[k].mat_id;
+            const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
+            if (dj < dbest || (dj == dbest && j > jbest)) { dbest = dj; mbest = mid; jbest = j; }
+            if (dj != dj && j > jnan) { jnan = j; mnan = mid; }
+        }
+        i = skip;
+    }
+    return v2(dbest, jnan > jbest ? mnan : mbest);
+}
+
 template <int NP>
 struct TableMap {
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
+        else if constexpr (NP == -2) return map_bvh(P, p);
         else return map_general(P, p);
     }
 };
