@@ -41,7 +41,7 @@ typedef struct rmr_params {
     int32_t max_bounces;       /* 16                                                          */
     float   step_multiply;     /* 0.5                                                         */
     int32_t separate_channels; /* 0                                                           */
-    int32_t use_env_tex;       /* 0 (env-map sky is not supported yet: RMR_E_UNSUPPORTED)     */
+    int32_t use_env_tex;       /* 0 (Graphics.cpp:338); 1 = skyColor from the env map          */
 } rmr_params;
 
 /* Kernel statistics for the roofline (accumulated since the last rmr_reset_stats). */
@@ -155,6 +155,11 @@ int rmr_reset_stats(rmr_ctx* ctx);
 int rmr_get_section_cycles(rmr_ctx* ctx, uint64_t out[4]);
 /* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */
 int rmr_set_kernel(rmr_ctx* ctx, int kernel);
+/* envTex of skyColor (RM1:78-113, RM2:84-107; the reference loads veranda_1k.hdr through SOIL as
+ * an RGBA8 texture, Graphics.cpp:287): w x h RGBA8 texels, row 0 = texture coordinate t = 0 (the
+ * direction +y). Used when params.use_env_tex != 0; NULL removes it. Sampling: bilinear, level 0,
+ * CLAMP_TO_EDGE. */
+int rmr_set_env_map(rmr_ctx* ctx, const uint8_t* rgba8, int w, int h);
 /* Per-scene kernel specialisation (the reference recompiles its shader per scene, Graphics::Reload):
  * the scene's map() is generated as HIP source with the primitives as literals and compiled by
  * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under

@@ -55,6 +55,7 @@ GLF(PFNGLUNIFORM3FPROC, glUniform3f)
 GLF(PFNGLUNIFORM4FPROC, glUniform4f)
 GLF(PFNGLGENTEXTURESPROC, glGenTextures)
 GLF(PFNGLBINDTEXTUREPROC, glBindTexture)
+GLF(PFNGLACTIVETEXTUREPROC, glActiveTexture)
 GLF(PFNGLTEXIMAGE2DPROC, glTexImage2D)
 GLF(PFNGLTEXPARAMETERIPROC, glTexParameteri)
 GLF(PFNGLBINDIMAGETEXTUREPROC, glBindImageTexture)
@@ -119,7 +120,7 @@ int main(int argc, char** argv) {
     LOAD(glGetShaderInfoLog); LOAD(glCreateProgram); LOAD(glAttachShader); LOAD(glLinkProgram);
     LOAD(glGetProgramiv); LOAD(glGetProgramInfoLog); LOAD(glUseProgram); LOAD(glGetUniformLocation);
     LOAD(glUniform1f); LOAD(glUniform1i); LOAD(glUniform3f); LOAD(glUniform4f); LOAD(glGenTextures);
-    LOAD(glBindTexture); LOAD(glTexImage2D); LOAD(glTexParameteri); LOAD(glBindImageTexture);
+    LOAD(glBindTexture); LOAD(glActiveTexture); LOAD(glTexImage2D); LOAD(glTexParameteri); LOAD(glBindImageTexture);
     LOAD(glDispatchCompute); LOAD(glMemoryBarrier); LOAD(glFinish); LOAD(glGetTexImage);
     LOAD(glGetString); LOAD(glGenBuffers); LOAD(glBindBuffer); LOAD(glBufferData);
     LOAD(glBindBufferBase); LOAD(glGetBufferSubData); LOAD(glGetError);
@@ -156,7 +157,7 @@ int main(int argc, char** argv) {
     for (char* line = strtok(job, "\n"); line; line = strtok(NULL, "\n")) {
         char name[128];
         float a, b, c, d;
-        int i0;
+        int i0, ew, eh;
         if (sscanf(line, "image %d %d", &W, &H) == 2) {
             float* zero = calloc((size_t)W * H * 4, sizeof(float));
             p_glGenTextures(1, &tex);
@@ -171,6 +172,21 @@ int main(int argc, char** argv) {
             p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA32F, 1, 1, 0, GL_RGBA, GL_FLOAT, one);
             p_glBindImageTexture(1, mtex, 0, GL_FALSE, 0, GL_READ_WRITE, GL_RGBA32F);
             free(zero);
+        } else if (sscanf(line, "envtex %127s %d %d", name, &ew, &eh) == 3) {
+            /* envTex sampler (texture unit 0): RGBA8, bilinear, clamp to edge, no mipmaps */
+            long n = 0;
+            char* data = slurp(name, &n);
+            if (n != (long)ew * eh * 4) { fprintf(stderr, "envtex size mismatch\n"); return 1; }
+            GLuint et = 0;
+            p_glActiveTexture(GL_TEXTURE0);
+            p_glGenTextures(1, &et);
+            p_glBindTexture(GL_TEXTURE_2D, et);
+            p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA8, ew, eh, 0, GL_RGBA, GL_UNSIGNED_BYTE, data);
+            p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MIN_FILTER, GL_LINEAR);
+            p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MAG_FILTER, GL_LINEAR);
+            p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_WRAP_S, GL_CLAMP_TO_EDGE);
+            p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_WRAP_T, GL_CLAMP_TO_EDGE);
+            free(data);
         } else if (sscanf(line, "uf %127s %f", name, &a) == 2) {
             p_glUniform1f(p_glGetUniformLocation(prog, name), a);
         } else if (sscanf(line, "ui %127s %d", name, &i0) == 2) {

@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 from oracle import camera  # noqa: E402
+from oracle.envmap import synthetic_env  # noqa: E402
 from oracle.glsl_ref import ref_run, shader_build  # noqa: E402
 from raymarchrenderer_amd import abi, parity_schedule, time_schedule  # noqa: E402
 
@@ -38,6 +39,9 @@ IMAGES = {
     "rm1_default": (os.path.join(GS, "default.scene"), 1, {}, 131072),
     "rm1_glass": (os.path.join(GS, "glass_test.scene"), 1, {}, 65536),
     "rm1_multilight": (os.path.join(GS, "multilight.scene"), 1, {}, 65536),
+    # env-map sky (useEnvTex = 1, synthetic_env): RM1:78-113 / RM2:84-107
+    "rm1_sphere1_env": (os.path.join(ROOT, "scenes", "sphere1.scene"), 1, {"max_bounces": 4, "use_env_tex": 1}, 16384),
+    "rm2_simple_env": (os.path.join(GS, "simple.scene"), 2, {"use_env_tex": 1}, 16384),
 }
 KATS = {
     "rm3": (None, 3),
@@ -131,13 +135,15 @@ def make_image(name, path, variant, kw, conv_spp, threads):
     scene = _scene(path)
     prm = abi.default_params(**kw)
     view = camera.default_view(W, H)
-    lo = ref_run.render(variant, scene, W, H, time_schedule(4), prm, view, threads=threads)
+    env = synthetic_env() if kw.get("use_env_tex") else None
+    lo = ref_run.render(variant, scene, W, H, time_schedule(4), prm, view, threads=threads, env=env)
     t0 = time.time()
     # converged reference on the parity schedule (small seeds, see raymarchrenderer_amd.parity_schedule)
-    conv = ref_run.render(variant, scene, W, H, parity_schedule(conv_spp), prm, view, threads=threads)
+    conv = ref_run.render(variant, scene, W, H, parity_schedule(conv_spp), prm, view, threads=threads, env=env)
     dt = time.time() - t0
+    extra = {"env": env} if env is not None else {}
     np.savez_compressed(os.path.join(GOLDEN, "img_%s.npz" % name), lo=lo, conv=conv, view=view,
-                        spp_lo=np.int32(4), spp_conv=np.int32(conv_spp), conv_schedule="parity")
+                        spp_lo=np.int32(4), spp_conv=np.int32(conv_spp), conv_schedule="parity", **extra)
     return dt
 
 

@@ -27,10 +27,13 @@ def ensure_built():
         subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+SHADER_CACHE = os.path.join(tempfile.gettempdir(), "rmr_glsl_ref")  # outside the repo: never shipped
+
+
 def _write_shader(src):
-    os.makedirs(REF_OUT, exist_ok=True)
+    os.makedirs(SHADER_CACHE, exist_ok=True)
     h = hashlib.sha1(src.encode()).hexdigest()[:16]
-    p = os.path.join(REF_OUT, "shader_%s.glsl" % h)
+    p = os.path.join(SHADER_CACHE, "shader_%s.glsl" % h)
     if not os.path.exists(p):
         with open(p, "w") as f:
             f.write(src)
@@ -41,13 +44,14 @@ def _uniform_lines(params, view):
     v = np.asarray(view, np.float32).reshape(5, 3)
     lines = ["uf maxDist %r" % float(params.max_dist), "ui maxSteps %d" % params.max_steps,
              "ui maxBounces %d" % params.max_bounces, "uf stepMultiply %r" % float(params.step_multiply),
-             "ui useEnvTex 0", "ui separateChannels %d" % params.separate_channels, "ui envTex 0"]
+             "ui useEnvTex %d" % params.use_env_tex, "ui separateChannels %d" % params.separate_channels,
+             "ui envTex 0"]
     for name, row in zip(["eye", "ray00", "ray01", "ray10", "ray11"], v):
         lines.append("u3f %s %.9g %.9g %.9g" % (name, row[0], row[1], row[2]))
     return lines
 
 
-def run_job(src, job_lines, out_floats_shape, ssbo_in=None, ssbo_out_n=0, threads=None, timeout=3600):
+def run_job(src, job_lines, out_floats_shape, ssbo_in=None, ssbo_out_n=0, threads=None, timeout=3600, env=None):
     ensure_built()
     shader = _write_shader(src)
     with tempfile.TemporaryDirectory() as td:
@@ -59,6 +63,10 @@ def run_job(src, job_lines, out_floats_shape, ssbo_in=None, ssbo_out_n=0, thread
             lines.insert(1, "ssbo_in %s" % pin)
         if ssbo_out_n:
             lines.insert(1, "ssbo_out %d" % ssbo_out_n)
+        if env is not None:  # after the "image" line, which binds the accumulator on unit 0
+            pe = os.path.join(td, "env.rgba8")
+            np.ascontiguousarray(env, np.uint8).tofile(pe)
+            lines.insert(1, "envtex %s %d %d" % (pe, env.shape[1], env.shape[0]))
         with open(job, "w") as f:
             f.write("\n".join(lines) + "\n")
         out = os.path.join(td, "out.f32")
@@ -76,7 +84,7 @@ def run_job(src, job_lines, out_floats_shape, ssbo_in=None, ssbo_out_n=0, thread
     return img, so
 
 
-def render(variant, scene, W, H, times, params, view, rect=None, first_sample=0, threads=None):
+def render(variant, scene, W, H, times, params, view, rect=None, first_sample=0, threads=None, env=None):
     """nspp Graphics::Render calls (one per entry of `times`, currentSample = first_sample + k) over
     `rect` (x0, y0, x1, y1) of a W x H accumulator that starts at 0. Returns (H, W, 4) float32."""
     src = shader_build.build(variant, scene)
@@ -86,7 +94,7 @@ def render(variant, scene, W, H, times, params, view, rect=None, first_sample=0,
     lines = ["image %d %d" % (W, H)] + _uniform_lines(params, view)
     for k, t in enumerate(times):
         lines.append("run %.9g %d %d %d %d %d %d %d" % (float(t), first_sample + k, x0, y0, x1, y1, gx, gy))
-    img, _ = run_job(src, lines, (H, W, 4), threads=threads)
+    img, _ = run_job(src, lines, (H, W, 4), threads=threads, env=env)
     return img
 
 

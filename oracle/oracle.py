@@ -53,13 +53,15 @@ def _fp(a):
 
 class Job(C.Structure):
     _fields_ = [("scene", C.POINTER(abi.Scene)), ("params", abi.Params), ("view", C.c_float * 15),
-                ("W", C.c_int), ("H", C.c_int)]
+                ("W", C.c_int), ("H", C.c_int), ("env", C.POINTER(C.c_float)), ("env_w", C.c_int),
+                ("env_h", C.c_int)]
 
 
 class Oracle:
     """One scene + params + view + image size, mirroring the GL state the reference renders with."""
 
-    def __init__(self, tables, params, view, W, H):
+    def __init__(self, tables, params, view, W, H, env=None):
+        """env: optional envTex as an (h, w, 4) uint8 RGBA texture (used when params.use_env_tex)."""
         self.tables = tables
         self.scene = tables.to_ctypes()
         self.job = Job()
@@ -67,6 +69,11 @@ class Oracle:
         self.job.params = params
         self.job.view[:] = [float(x) for x in np.asarray(view, np.float32).reshape(15)]
         self.job.W, self.job.H = W, H
+        if env is not None:
+            env = np.asarray(env, np.uint8)
+            self._env = np.ascontiguousarray(env.astype(np.float32) / np.float32(255.0))  # GL unorm8
+            self.job.env = self._env.ctypes.data_as(C.POINTER(C.c_float))
+            self.job.env_h, self.job.env_w = env.shape[:2]
         self.W, self.H = W, H
         self.map_evals = 0
 

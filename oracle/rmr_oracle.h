@@ -26,6 +26,10 @@ typedef struct oracle_job {
     rmr_params params;
     float view[15];
     int W, H;
+    /* envTex (used when params.use_env_tex != 0): env_w x env_h RGBA texels as floats, row 0 = t 0,
+     * i.e. the RGBA8 texture's c / 255 (GL unorm conversion) */
+    const float* env;
+    int env_w, env_h;
 } oracle_job;
 
 /* Radiance of one sample of pixel (px,py) at seed `time` — RayMarch*.glsl main() minus the

@@ -20,7 +20,7 @@ EXPORTS = [
     "rmr_render_spp", "rmr_render_tiles", "rmr_read_accum", "rmr_write_accum",
     "rmr_accum_device_ptr", "rmr_bind_accum", "rmr_save_bmp", "rmr_encode_bmp",
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats", "rmr_get_section_cycles",
-    "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_jit_compile_scene",
+    "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_jit_compile_scene", "rmr_set_env_map",
     "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free",
 ]
 
@@ -81,6 +81,7 @@ def lib():
         "rmr_set_kernel": (C.c_int, [vp, C.c_int]),
         "rmr_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_longlong]),
         "rmr_set_jit": (C.c_int, [vp, C.c_int]),
+        "rmr_set_env_map": (C.c_int, [vp, C.c_void_p, C.c_int, C.c_int]),
         "rmr_jit_compile_scene": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
         "rmr_trace_samples": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, fp]),
         "rmr_abi_sizes": (C.c_int, [C.POINTER(C.c_int32), C.c_int]),

@@ -56,6 +56,8 @@ struct rmr_ctx {
     rmr::DPrim* d_dprims = nullptr;
     rmr::DMat* d_dmats = nullptr;
     rmr::BvhNode* d_bvh = nullptr;
+    float4* d_env = nullptr;              // envTex (rmr_set_env_map)
+    int env_w = 0, env_h = 0;
     int n_bvh = 0;
     float bvh_margin = 1e-4f;
     int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
@@ -416,7 +418,7 @@ int collect_timing(rmr_ctx* c) {
 int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, int x1, int y1,
                  const float* times, uint32_t first_sample, uint32_t nspp) {
     if (!c->scene_loaded) return fail(c, RMR_E_STATE, "no scene loaded (call rmr_load_scene_json / rmr_load_builtin_scene)");
-    if (c->params.use_env_tex) return fail(c, RMR_E_UNSUPPORTED, "useEnvTex != 0 is not supported");
+    if (c->params.use_env_tex && !c->d_env) return fail(c, RMR_E_STATE, "useEnvTex != 0 but no env map (rmr_set_env_map)");
     if (tiles.empty() || nspp == 0) return RMR_OK;
     if (!c->view_set) default_view(c);
     int r;
@@ -445,6 +447,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
     P.spec_sky = s.spectral_sky;
+    P.env = c->d_env; P.env_w = c->env_w; P.env_h = c->env_h;
+    P.use_env = (c->params.use_env_tex != 0 && c->d_env) ? 1 : 0;
     for (int i = 0; i < 3; i++) { P.sky[i] = s.sky[i]; P.rm2_light[i] = s.rm2.light_pos[i]; }
     P.rm2_light_power = s.rm2.light_power;
     P.rm2_node_id = s.rm2.node_mat_id;
@@ -574,7 +578,7 @@ void rmr_destroy(rmr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
-    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_samp,
+    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_env, c->d_samp,
                     c->d_tiles, c->d_times, c->d_queue, c->d_counters};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -853,6 +857,26 @@ int rmr_reset_stats(rmr_ctx* c) {
 int rmr_set_kernel(rmr_ctx* c, int kernel) {
     if (!c || kernel < 0 || kernel > 1) return RMR_E_INVALID;
     c->kernel_mode = kernel;
+    return RMR_OK;
+}
+
+int rmr_set_env_map(rmr_ctx* c, const uint8_t* rgba8, int w, int h) {
+    if (!c) return RMR_E_INVALID;
+    if (!rgba8) {
+        if (c->d_env) (void)hipFree(c->d_env);
+        c->d_env = nullptr;
+        c->env_w = c->env_h = 0;
+        return RMR_OK;
+    }
+    if (w <= 0 || h <= 0 || (size_t)w * h > ((size_t)1 << 26)) return fail(c, RMR_E_INVALID, "bad env map size");
+    std::vector<float4> t((size_t)w * h);
+    for (size_t i = 0; i < t.size(); i++)  // GL unorm8 -> float: c / 255
+        t[i] = make_float4((float)rgba8[4 * i] / 255.0f, (float)rgba8[4 * i + 1] / 255.0f,
+                           (float)rgba8[4 * i + 2] / 255.0f, (float)rgba8[4 * i + 3] / 255.0f);
+    int r;
+    if ((r = dev_upload(c, &c->d_env, t.data(), t.size()))) return r;
+    c->env_w = w;
+    c->env_h = h;
     return RMR_OK;
 }
 

@@ -64,6 +64,8 @@ struct KParams {
     int32_t v2_begin, v2_end;
     rmr_spectral spec_sky;
     float sky[3];
+    const float4* env;          // envTex texels (c / 255, RGBA), row 0 = t 0; used when use_env
+    int32_t env_w, env_h, use_env;
     float rm2_light[3];
     float rm2_light_power;
     int32_t rm2_node_id;

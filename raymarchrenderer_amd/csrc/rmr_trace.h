@@ -391,6 +391,30 @@ RMR_D float gray_ch(V3 c, int chan) {
 
 #define PH_DONE (-1)
 
+// skyColor(dir), RM1:78-113 = RM2:84-107: constant 0.015, or with useEnvTex the equirectangular
+// envTex lookup, texture2D restated as GL's bilinear filter at level 0 with CLAMP_TO_EDGE (same
+// arithmetic as the oracle's sky_color; the reference driver's filter precision is its own).
+RMR_D V3 sky_color(const KParams& P, V3 dir) {
+    if (!P.use_env) return v3(P.sky[0], P.sky[1], P.sky[2]);
+    const float PI = 3.141592653f;
+    float phi = det_atan2(dir.z, dir.x);
+    if (phi < 0.0f) phi += 2.0f * PI;
+    const float s = phi / (2.0f * PI);
+    const float t = 1.0f - (dir.y * 0.5f + 0.5f);
+    const int W = P.env_w, H = P.env_h;
+    const float fu = s * (float)W - 0.5f, fv = t * (float)H - 0.5f;
+    const float i0f = floorf(fu), j0f = floorf(fv);
+    const float a = fu - i0f, b = fv - j0f;
+    const int i0 = (int)fminf(fmaxf(i0f, 0.0f), (float)(W - 1)), i1 = (int)fminf(fmaxf(i0f + 1.0f, 0.0f), (float)(W - 1));
+    const int j0 = (int)fminf(fmaxf(j0f, 0.0f), (float)(H - 1)), j1 = (int)fminf(fmaxf(j0f + 1.0f, 0.0f), (float)(H - 1));
+    const float4 t00 = P.env[(size_t)j0 * W + i0], t10 = P.env[(size_t)j0 * W + i1];
+    const float4 t01 = P.env[(size_t)j1 * W + i0], t11 = P.env[(size_t)j1 * W + i1];
+    const float ia = 1.0f - a, ib = 1.0f - b;
+    const V3 top = v3(t00.x * ia + t10.x * a, t00.y * ia + t10.y * a, t00.z * ia + t10.z * a);
+    const V3 bot = v3(t01.x * ia + t11.x * a, t01.y * ia + t11.y * a, t01.z * ia + t11.z * a);
+    return v3(top.x * ib + bot.x * b, top.y * ib + bot.y * b, top.z * ib + bot.z * b);
+}
+
 template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
     L.t = 0.0f;
@@ -880,7 +904,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
         }
         if (want) rm1_after_material<HO>(P, L, nc, nd, ni, nh);
         if (L.phase == PH_MISS) {  // shader_emission(ray, skyColor(dir), vec3(1), emit), RM1:555-561
-            const V3 emit = v3(P.sky[0], P.sky[1], P.sky[2]) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
+            const V3 emit = sky_color(P, L.d) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
             L.color = L.color * emit;
             if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
@@ -937,7 +961,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
             }
         } else if (L.phase == PH_MISS) {
-            L.color = L.color * v3(P.sky[0], P.sky[1], P.sky[2]);
+            L.color = L.color * sky_color(P, L.d);   // RM2:509
             if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
     }

@@ -123,6 +123,9 @@ rmr_params Graphics::getParams() {
     return p;
 }
 void Graphics::setDevice(int device) { g_device = device; }
+void Graphics::setEnvMap(const unsigned char* rgba8, int w, int h) {
+    if (need_ctx("setEnvMap")) check(rmr_set_env_map(g_ctx, rgba8, w, h), "setEnvMap");
+}
 void Graphics::Sync() {
     if (need_ctx("Sync")) check(rmr_sync(g_ctx), "Sync");
 }

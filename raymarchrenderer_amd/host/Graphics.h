@@ -46,6 +46,9 @@ public:
     static void setParams(const rmr_params& p);
     static rmr_params getParams();
     static void setDevice(int device);
+    // envTex of skyColor (Graphics.cpp:287 loads it from data/textures/veranda_1k.hdr): RGBA8, row
+    // 0 = up; used when the params' use_env_tex is set. nullptr removes it.
+    static void setEnvMap(const unsigned char* rgba8, int w, int h);
     static void Sync();
     static bool saveCheckpoint(const std::string& path, unsigned samplesDone);
     static bool loadCheckpoint(const std::string& path, unsigned* samplesDone);

@@ -40,7 +40,8 @@ namespace {
 const float PI = 3.141592653f;  // Program.cpp:62
 
 struct Options {
-    std::string scene, out, checkpoint, resume, scene_dir = "scenes";
+    std::string scene, out, checkpoint, resume, scene_dir = "scenes", env_map;
+    int env_w = 0, env_h = 0;
     int variant = -1;
     int width = 800, height = 600;  // Graphics.cpp:6
     int samples = 128;              // Program.cpp:104
@@ -305,6 +306,7 @@ void usage() {
         "  --grid GWxGH        tile grid (default 4x4)\n"
         "  --bounces B --max-steps N --max-dist D --step-mult S --separate-channels 0|1\n"
         "  --camera ex,ey,ez,dx,dy,dz   (default 0,4,-6,0,-3,6)\n"
+        "  --env-map FILE WxH  raw RGBA8 envTex for skyColor (row 0 = up); enables useEnvTex\n"
         "  --frame F           seed schedule frame: time = 1000 F + 0.016 s\n"
         "  --per-sample        one Graphics::Render launch per sample per tile (reference pattern)\n"
         "  --out FILE.bmp      (default output/<timestamp>.bmp)\n"
@@ -353,6 +355,11 @@ bool parse(int argc, char** argv, Options& o) {
         else if (a == "--interactive") o.interactive = true;
         else if (a == "--scene-dir") o.scene_dir = next("--scene-dir");
         else if (a == "--quiet") o.quiet = true;
+        else if (a == "--env-map") {  // raw RGBA8 file + its size: skyColor's envTex, enables useEnvTex
+            o.env_map = next("--env-map");
+            if (std::sscanf(next("--env-map size"), "%dx%d", &o.env_w, &o.env_h) != 2) return false;
+            o.params.use_env_tex = 1;
+        }
         else if (a == "--print-tiles") o.print_tiles = true;
         else if (a == "--print-view") o.print_view = true;
         else if (a == "--help" || a == "-h") {
@@ -398,6 +405,15 @@ int main(int argc, char** argv) {
     if (!Graphics::context()) return 3;  // no device: fail loudly, there is no CPU path
     if (!o.interactive && Graphics::lastStatus() != RMR_OK) return 1;  // interactive: scene comes later
     Graphics::setParams(o.params);
+    if (!o.env_map.empty()) {
+        bool ok = false;
+        const std::string tex = read_file(o.env_map, &ok);
+        if (!ok || tex.size() != (size_t)o.env_w * o.env_h * 4) {
+            std::cerr << "env map: cannot read " << o.env_w << "x" << o.env_h << " RGBA8 from " << o.env_map << std::endl;
+            return 1;
+        }
+        Graphics::setEnvMap((const unsigned char*)tex.data(), o.env_w, o.env_h);
+    }
     if (o.interactive) return interactive(o);
     const RenderResult r = render(o, 0);
     if (Graphics::lastStatus() != RMR_OK) return 1;

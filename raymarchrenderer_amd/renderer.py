@@ -153,6 +153,15 @@ class Renderer:
     def set_tuning(self, shade_threshold=0, grid_per_cu=-1, samp_budget=0):
         _check(self._ctx, lib().rmr_set_tuning(self._ctx, int(shade_threshold), int(grid_per_cu), int(samp_budget)))
 
+    def set_env_map(self, rgba8):
+        """envTex for skyColor (used with params use_env_tex=1): (h, w, 4) uint8, row 0 = up. None clears."""
+        if rgba8 is None:
+            _check(self._ctx, lib().rmr_set_env_map(self._ctx, None, 0, 0))
+            return
+        a = np.ascontiguousarray(rgba8, np.uint8)
+        self._env = a
+        _check(self._ctx, lib().rmr_set_env_map(self._ctx, a.ctypes.data, a.shape[1], a.shape[0]))
+
     def set_jit(self, mode):
         """hipRTC per-scene kernel specialisation: 0 off, 1 always, 2 auto (large launches)."""
         _check(self._ctx, lib().rmr_set_jit(self._ctx, int(mode)))

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from oracle import camera, oracle, scene_compile
+from oracle.envmap import synthetic_env
 from raymarchrenderer_amd import abi, time_schedule
 
 from .conftest import GOLDEN, SCENES
@@ -32,6 +33,9 @@ CASES = [
     ("rm1_cornell5_steps", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 3, "max_steps": 40}),
     ("rm1_mandelbulb_b2", os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}),
     ("rm1_csg256_b4", os.path.join(SCENES, "csg256.scene"), "rm1", {"max_bounces": 4}),
+    ("rm1_sphere1_env", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
+    ("rm1_default_env", os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {"use_env_tex": 1}),
+    ("rm2_simple_env", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}),
 ]
 
 
@@ -52,6 +56,7 @@ def _setup(r, path, variant, W, H, overrides):
     r.set_params(prm)
     view = camera.default_view(W, H)
     r.set_view(view)
+    r.set_env_map(synthetic_env() if prm.use_env_tex else None)
     return prm, view
 
 
@@ -69,7 +74,7 @@ def test_samples_bitexact(renderer, name, path, variant, overrides):
     prm, view = _setup(renderer, path, variant, W, H, overrides)
     times = time_schedule(3, frame=1)
     gpu = renderer.trace_samples(times, rect)
-    orc = oracle.Oracle(_tables(path, variant), prm, view, W, H)
+    orc = oracle.Oracle(_tables(path, variant), prm, view, W, H, env=synthetic_env() if prm.use_env_tex else None)
     cpu = orc.trace_samples(times, rect)
     eq = same_bits(gpu[..., :3], cpu[..., :3])
     bad = np.argwhere(~eq.all(axis=-1))

@@ -32,6 +32,8 @@ CASES = {
     "rm1_glass": (os.path.join(GOLDEN, "scenes", "glass_test.scene"), "rm1", {}, 40.0),
     "rm1_multilight": (os.path.join(GOLDEN, "scenes", "multilight.scene"), "rm1", {}, 40.0),
     "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}, 40.0),
+    "rm1_sphere1_env": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}, 40.0),
+    "rm2_simple_env": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}, 40.0),
 }
 
 
@@ -56,9 +58,13 @@ def test_converged_psnr_vs_reference(renderer, name):
         renderer.load_scene(path, variant)
     renderer.set_params(abi.default_params(**kw))
     renderer.set_view(g["view"])
+    renderer.set_env_map(g["env"] if "env" in g.files else None)
     n = n_ref
-    renderer.render_spp(parity_schedule(n))
-    img = renderer.read_accum()
+    try:
+        renderer.render_spp(parity_schedule(n))
+        img = renderer.read_accum()
+    finally:
+        renderer.set_env_map(None)
     p = psnr(img, ref)
     rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(ref[..., :3].mean(), 1e-12)
     print("%s: PSNR %.2f dB vs reference @%d spp (GPU %d spp), mean rel diff %+.4f" % (name, p, n_ref, n, rel))

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import camera, oracle, scene_compile
+from oracle.envmap import synthetic_env
 from raymarchrenderer_amd import abi, time_schedule
 from raymarchrenderer_amd.renderer import jit_compile_scene
 
@@ -22,12 +23,15 @@ SCENE_CASES = [
     ("rm1_csg256_b4", os.path.join(SCENES, "csg256.scene"), "rm1", {"max_bounces": 4}),
     ("rm2_simple", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {}),
     ("rm3_builtin", None, "rm3", {}),
+    ("rm1_sphere1_env", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
 ]
 IDS = [c[0] for c in SCENE_CASES]
 
 
 @pytest.mark.parametrize("name,path,variant,overrides", SCENE_CASES, ids=IDS)
 def test_jit_source_compiles_for_gfx950(tmp_path, monkeypatch, name, path, variant, overrides):
+    if name.endswith("_env"):
+        pytest.skip("same generated source as the scene without the env map (the sky is a kernel parameter)")
     monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path))
     key = jit_compile_scene(path, variant)
     assert len(key) == 16
@@ -47,6 +51,7 @@ def _setup(r, path, variant, W, H, overrides):
     r.set_params(prm)
     view = camera.default_view(W, H)
     r.set_view(view)
+    r.set_env_map(synthetic_env() if prm.use_env_tex else None)
     return prm, view
 
 
@@ -69,7 +74,8 @@ def test_jit_samples_bitexact_vs_oracle(renderer, name, path, variant, overrides
     finally:
         renderer.set_jit(2)
     assert st.jit_launches > 0
-    cpu = oracle.Oracle(_tables(path, variant), prm, view, W, H).trace_samples(times, rect)
+    env = synthetic_env() if prm.use_env_tex else None
+    cpu = oracle.Oracle(_tables(path, variant), prm, view, W, H, env=env).trace_samples(times, rect)
     a, b = gpu[..., :3], cpu[..., :3]
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), "%s: %d samples differ" % (name, (~same.all(-1)).sum())

@@ -103,6 +103,8 @@ IMAGES = {
     "rm1_glass": (os.path.join(GOLDEN, "scenes", "glass_test.scene"), "rm1", {}),
     "rm1_multilight": (os.path.join(GOLDEN, "scenes", "multilight.scene"), "rm1", {}),
     "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}),
+    "rm1_sphere1_env": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
+    "rm2_simple_env": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}),
 }
 
 
@@ -115,7 +117,8 @@ def test_image_statistics_vs_reference(name):
     g = np.load(os.path.join(GOLDEN, "img_%s.npz" % name))
     path, variant, kw = IMAGES[name]
     H, W = g["conv"].shape[:2]
-    o = oracle.Oracle(_tables(path, variant), abi.default_params(**kw), g["view"], W, H)
+    env = g["env"] if "env" in g.files else None
+    o = oracle.Oracle(_tables(path, variant), abi.default_params(**kw), g["view"], W, H, env=env)
     spp = 512
     x0, y0, x1, y1 = W // 4, H // 4, W // 4 + 32, H // 4 + 24
     n_ref = int(g["spp_conv"])
@@ -129,6 +132,9 @@ def test_image_statistics_vs_reference(name):
         return a.reshape(h // 4, 4, w // 4, 4, c).mean(axis=(1, 3))
     mb, rb = blocks(m), blocks(ref)
     se = np.sqrt(blocks(v) / 16.0 * (1.0 / spp + 1.0 / int(g["spp_conv"])))
+    # plus a 0.1 % systematic allowance: the driver's texture-filter precision (envTex) and sin() are
+    # implementation-defined (llvmpipe filters with 8-bit weights), visible where samples barely vary
+    se = np.sqrt(se ** 2 + (1e-3 * np.abs(blocks(ref))) ** 2)
     ok = se > 0
     z = (mb - rb)[ok] / se[ok]
     # blocks whose samples never vary (sky, shadow) may still see rare events in the 16k-64k
