@@ -627,10 +627,7 @@ RMR_D void normal_update(Lane& L, float m) {
     L.nrm.y = ax == 1 ? vy : L.nrm.y;
     L.nrm.z = ax == 2 ? vz : L.nrm.z;
     L.ctr++;
-    if (L.ctr == 6) {
-        L.nrm = normalize(L.nrm);
-        L.phase = PH_HIT;
-    }
+    if (L.ctr == 6) L.phase = PH_HIT;   // normalize() happens in the shading batch (shade())
 }
 
 // ------------------------------------------------------------------------------------------
@@ -874,6 +871,9 @@ RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) 
 template <int VAR, bool PROG, class MATS>
 RMR_D void shade(const KParams& P, Lane& L) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
+    // getNormal's normalize (RM1:267), deferred from the last probe to the batch: the map loop then
+    // carries no division/sqrt for the few lanes that finish a normal in a given iteration
+    if (L.phase == PH_HIT) L.nrm = normalize(L.nrm);
     if (VAR == RMR_VARIANT_RM1) {
         const bool want = (L.phase == PH_HIT);
         const int id = want ? (int)L.mid : -1;
