@@ -79,7 +79,7 @@ struct rmr_ctx {
     rmr_stats stats{};
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
     int shade_threshold = 16;
-    int refill_threshold = 8;   // 0 = shade_threshold (tuned on C2: T=16, refill at 8 idle lanes)
+    int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels)

@@ -570,6 +570,44 @@ RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
     }
 }
 
+// Primary rays of a work chunk, computed full-width by the wave that fetches the chunk (instead of
+// by the few lanes each refill starts) and kept in LDS: (dir.xyz, randChange after the 3 jitter
+// rand() calls) and (gid.x + time, gid.y + time, time, in clip rect).
+struct ChunkRay { float4 a, b; };
+RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
+    int px, py;
+    float time, rc = 0.0f;
+    ChunkRay r;
+    const bool in_rect = unit_pixel(P, u, px, py, time);
+    V3 dir = v3s(0.0f);
+    if (in_rect) dir = primary_dir(P, px, py, time, rc);
+    r.a = make_float4(dir.x, dir.y, dir.z, rc);
+    r.b = make_float4((float)px + time, (float)py + time, time, in_rect ? 1.0f : 0.0f);
+    return r;
+}
+// begin_trace for a fresh unit whose primary ray is in LDS
+template <int VAR, bool HO>
+RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b) {
+    if (b.w == 0.0f) {
+        L.phase = PH_IDLE;
+        return;
+    }
+    L.unit = u;
+    L.time = b.z;
+    L.gxt = b.x;
+    L.gyt = b.y;
+    L.rc = a.w;
+    L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
+    const V3 dir = v3(a.x, a.y, a.z);
+    for (;;) {  // a zero-bounce trace finishes at once (and may start the next channel)
+        if (trace_prologue<VAR, HO>(P, L, dir)) return;
+        if (finish_trace<VAR, HO>(P, L)) {
+            L.phase = PH_DONE;
+            return;
+        }
+    }
+}
+
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
 // distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
 template <bool HO>
@@ -1031,6 +1069,9 @@ RMR_D void trace_main(const KParams& P) {
 #else
 #define RMR_STAMP(v)
 #endif
+    __shared__ ChunkRay s_ray[4][CHUNK];   // per wave (256-thread blocks = 4 waves)
+    const int wv = (threadIdx.x >> 6) & 3;
+    uint32_t chunk_base = 0;
     for (;;) {
         RMR_STAMP(c0);
         bool fresh = false;
@@ -1046,6 +1087,13 @@ RMR_D void trace_main(const KParams& P) {
                     rnext = base;
                     exhausted = base >= n_units;
                     rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
+                    if (!exhausted) {  // the chunk's primary rays, all 64 lanes at once
+                        chunk_base = base;
+                        for (uint32_t sl = __lane_id(); sl < CHUNK; sl += 64) {
+                            if (base + sl < rend) s_ray[wv][sl] = chunk_ray(P, base + sl);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
                 }
                 if (!exhausted) {
                     const uint32_t avail = rend - rnext;
@@ -1062,8 +1110,18 @@ RMR_D void trace_main(const KParams& P) {
             }
         }
         const bool restart = (L.phase == PH_RESTART);
-        if (__ballot(fresh || restart)) {
-            if (fresh || restart) begin_trace<VAR, HO>(P, L, fresh ? fu : L.unit, fresh);
+        if (PERSIST) {
+            if (__ballot(fresh)) {
+                if (fresh) {
+                    const ChunkRay cr = s_ray[wv][fu - chunk_base];
+                    begin_unit<VAR, HO>(P, L, fu, cr.a, cr.b);
+                }
+            }
+            if (__ballot(restart)) {
+                if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
+            }
+        } else if (__ballot(restart)) {
+            if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
         }
         RMR_STAMP(c1);
         const bool act = is_active(L.phase);
