@@ -36,6 +36,12 @@ CASES = [
     ("rm1_sphere1_env", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
     ("rm1_default_env", os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {"use_env_tex": 1}),
     ("rm2_simple_env", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}),
+    # edge cases: zero bounces (trace() returns its throughput untouched), zero march steps (every
+    # march falls out of its loop: a miss), an empty scene, separateChannels on RM2
+    ("rm1_cornell5_b0", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 0}),
+    ("rm1_cornell5_steps0", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_steps": 0}),
+    ("rm1_empty", os.path.join(SCENES, "empty.scene"), "rm1", {}),
+    ("rm2_simple_sepch", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"separate_channels": 1}),
 ]
 
 
@@ -114,6 +120,34 @@ def test_render_single_sample_bounds(renderer):
     assert same_bits(gpu, cpu).all()
     assert (gpu[:3, :, :] == 0).all() and (gpu[:, :5, :] == 0).all()
     assert (gpu[3:18, 5:20, 3] == 1).all()
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (9, 17)])
+def test_tiny_and_ragged_images(renderer, W, H):
+    """Images smaller than one 8x8 tile or not a multiple of it: only in-image pixels are written."""
+    path = os.path.join(SCENES, "cornell5.scene")
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 2})
+    times = time_schedule(3)
+    renderer.render_spp(times)
+    gpu = renderer.read_accum()
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).render(times)
+    assert gpu.shape == (H, W, 4)
+    assert same_bits(gpu, cpu).all()
+
+
+def test_rect_clipping_and_empty_calls(renderer):
+    """A rect reaching outside the image is clipped; zero samples or an empty rect is a no-op."""
+    W, H = 24, 16
+    path = os.path.join(SCENES, "cornell5.scene")
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 2})
+    times = time_schedule(2)
+    renderer.render_spp(times[:0])
+    renderer.render_spp(times, rect=(5, 5, 5, 9))
+    assert (renderer.read_accum() == 0).all()
+    renderer.render_spp(times, rect=(-8, 10, 40, 30))
+    gpu = renderer.read_accum()
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).render(times, rect=(0, 10, W, H))
+    assert same_bits(gpu, cpu).all()
 
 
 def test_render_tiles_partition_sums_to_full(renderer):
