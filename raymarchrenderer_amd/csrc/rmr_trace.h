@@ -256,15 +256,6 @@ typedef const __attribute__((address_space(4))) int8v CInt8v;
 
 template <int NP>
 RMR_D V2 map_fixed(const KParams& P, V3 p) {
-#ifdef RMR_EXP_CORNELL  // experiment: scenes/cornell5.scene baked in as literals (JIT estimate)
-    V2 d = v2(P.max_dist, -1.0f);
-    opu(d, sd_box(p, v3(0.0f, -1.025f, 0.0f), v3(4.0f, 0.05f, 4.0f)), 0.0f);
-    opu(d, sd_box(p, v3(-3.0f, 1.0f, 0.0f), v3(0.05f, 3.0f, 4.0f)), 1.0f);
-    opu(d, sd_box(p, v3(3.0f, 1.0f, 0.0f), v3(0.05f, 3.0f, 4.0f)), 2.0f);
-    opu(d, sd_sphere(p, v3(0.0f, 0.0f, 0.0f), 1.0f), 0.0f);
-    opu(d, sd_box(p, v3(0.0f, 4.0f, 0.0f), v3(1.5f, 0.05f, 1.5f)), 3.0f);
-    return d;
-#else
     CInt8v* pr = (CInt8v*)P.dprims;
     V2 d = v2(P.max_dist, -1.0f);
     int8v cur = pr[0];
@@ -281,7 +272,6 @@ RMR_D V2 map_fixed(const KParams& P, V3 p) {
         if (j + 1 < NP) cur = nxt;
     }
     return d;
-#endif
 }
 
 RMR_D V2 map_loop(const KParams& P, V3 p) {
