@@ -88,6 +88,9 @@ struct rmr_ctx {
     bool jit_ready = false;     // `jit` matches the loaded scene
     bool jit_failed = false;    // compile/load failed for the loaded scene (auto mode falls back)
     rmr::JitKernel jit;
+    std::string jit_struct_src;  // structure-only source of the last specialised scene
+    std::string jit_baked_src;   // its baked source
+    bool jit_bake = true;        // false once a reload only moved primitives (animation)
     std::vector<rmr::JitKernel> jit_loaded;  // modules loaded by this context (unloaded at destroy)
     size_t samp_budget = (size_t)8 << 30;
     std::string err;
@@ -208,7 +211,15 @@ int upload_scene(rmr_ctx* c) {
 // Compile (or fetch from the cache) and load the specialised trace kernel of the loaded scene.
 int ensure_jit(rmr_ctx* c) {
     if (c->jit_ready) return RMR_OK;
-    const std::string src = rmr::jit_source(c->scene, c->has_prog);
+    // animation: same structure as the last specialised scene, different numbers -> stop baking the
+    // numbers for this context (one structure-only kernel instead of a compile per frame)
+    const std::string struct_src = rmr::jit_source(c->scene, c->has_prog, false);
+    const std::string baked_src = rmr::jit_source(c->scene, c->has_prog, true);
+    if (struct_src != c->jit_struct_src) c->jit_bake = true;                        // new layout
+    else if (baked_src != c->jit_baked_src && !c->jit_baked_src.empty()) c->jit_bake = false;  // moved
+    c->jit_struct_src = struct_src;
+    c->jit_baked_src = baked_src;
+    const std::string& src = c->jit_bake ? baked_src : struct_src;
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {

@@ -96,3 +96,28 @@ def test_jit_matches_table_kernel_on_large_render(renderer):
         assert (renderer.stats().jit_launches > 0) == (mode == 1)
     renderer.set_jit(2)
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_jit_animated_scene_bitexact(renderer):
+    """C5-style animation: a reload that only moves a primitive switches the context to the
+    structure-only kernel (no per-frame compile); every frame still equals the table kernel."""
+    import json
+    import math
+    W, H = 64, 48
+    with open(os.path.join(SCENES, "cornell5.scene")) as f:
+        base = json.load(f)
+    times = time_schedule(4)
+    for frame in range(3):
+        sc = json.loads(json.dumps(base))
+        sc["objects"][3]["nodes"][0]["inputs"][1][1] = 0.5 * math.sin(2.0 * math.pi * frame / 120.0)
+        out = {}
+        for mode in (1, 0):
+            renderer.set_jit(mode)
+            _setup(renderer, sc, "rm1", W, H, {"max_bounces": 4})
+            renderer.reset_stats()
+            renderer.render_spp(times)
+            out[mode] = renderer.read_accum()
+            assert (renderer.stats().jit_launches > 0) == (mode == 1)
+        assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)), "frame %d" % frame
+    renderer.set_jit(2)

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 python bench.py > gpurun_out/bench_c2.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_c2.log
 for c in c1 c3 c5; do
-  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_$c.log 2>&1 || exit $?
+  timeout -k 10 300 python bench.py --config $c --warmup 2 --no-cpu-baseline > gpurun_out/bench_$c.log 2>&1 || exit $?
   tail -1 gpurun_out/bench_$c.log | cut -c1-330
 done
 timeout -k 10 400 python bench.py --config c4 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c4.log 2>&1 || exit $?
