@@ -455,6 +455,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.dprims = c->d_dprims; P.dmats = c->d_dmats;
     P.bvh = c->d_bvh; P.n_nodes = c->n_bvh; P.bvh_margin = c->bvh_margin;
     P.n_prims = (int)s.prims.size();
+    P.am_r2 = 2.0f * rmr::max_sphere_radius(s);
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
     P.spec_sky = s.spectral_sky;

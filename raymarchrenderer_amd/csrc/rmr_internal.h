@@ -59,6 +59,7 @@ struct KParams {
     const BvhNode* bvh;         // NP = -2: node array (n_nodes), prims in dprims in leaf order
     int32_t n_nodes;
     float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)
+    float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     int32_t n_prims;
     int32_t n_mats;
     int32_t v2_begin, v2_end;

@@ -248,6 +248,61 @@ RMR_D void opu_sphere_culled(V2& d, V3 p, V3 c, float r, float mid) {
 }
 
 
+// Approximate-then-exact map() for sphere/box scenes (bit-identical to the opU fold above).
+// Every primitive's distance is first formed with the bare v_sqrt_f32 (within 1 ulp of the
+// correctly rounded sqrt for x >= 2^-96 — the premise sqrt_cr's fix-up is proven on, exhaustively —
+// and within 2^-47 absolutely below) instead of sqrt_cr's 10-instruction fix-up and tiny-input
+// branch. The fold tracks the approximate minimum a (first index on equal values), the
+// second-smallest value s2 (one v_med3), and the minimiser's (len2, k) with d = RN(sqrt(len2) + k):
+// box k = min(max q, 0) (sd_box = k + length(max(q, 0))), sphere k = -r. Error of an approximate
+// distance: |a_j - d_j| <= 2^-21 (|a_j| + R) + 2^-40, R = the largest |sphere radius| (a sphere's
+// sqrt is d + r). If s2 - a exceeds both minimisers' bounds (am_margin, with 2x slack), every other
+// primitive's exact distance is strictly above the minimiser's, so the fold's closed form
+// (map_bvh) is opU((maxDist, -1), exact d_w, id_w): one sqrt_cr per map() instead of one
+// per primitive. Lanes where it is not (near ties, NaN p) run the exact fold (wave-uniform branch).
+struct AMin {
+    float a, s2, l2, k, id;
+};
+RMR_D void am_init(AMin& m) {
+    m.a = __builtin_inff();
+    m.s2 = __builtin_inff();
+    m.l2 = 0.0f;
+    m.k = 0.0f;
+    m.id = -1.0f;
+}
+RMR_D void am_take(AMin& m, float a, float l2, float k, float id) {
+    m.s2 = __builtin_amdgcn_fmed3f(m.a, a, m.s2);
+    const bool t = a < m.a;
+    m.a = t ? a : m.a;
+    m.l2 = t ? l2 : m.l2;
+    m.k = t ? k : m.k;
+    m.id = t ? id : m.id;
+}
+RMR_D void am_box(AMin& m, V3 p, V3 c, V3 r, float id) {
+    const V3 q = vabs(p - c) - r;
+    const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
+    const V3 o = vmax0(q);
+    const float l2 = dot(o, o);
+    am_take(m, k + __builtin_amdgcn_sqrtf(l2), l2, k, id);
+}
+RMR_D void am_sphere(AMin& m, V3 p, V3 c, float r, float id) {
+    const V3 v = p - c;
+    const float l2 = dot(v, v);
+    am_take(m, __builtin_amdgcn_sqrtf(l2) - r, l2, -r, id);
+}
+// true when the minimiser is certain (see above); false for near ties, NaN and infinite values
+RMR_D bool am_unique(const AMin& m, float R2) {   // R2 = 2 R
+    const float margin = fmaf(fabsf(m.a) + fabsf(m.s2) + R2, 0x1p-20f, 0x1p-39f);
+    return m.s2 - m.a > margin;
+}
+// exact result of a unique fold: opU((maxDist, -1), d_w, id_w); d_w = sqrt_cr(len2) + k is the same
+// expression as sd_box (k + length) and sd_sphere (length - r == length + (-r)).
+RMR_D V2 am_result(const KParams& P, const AMin& m) {
+    V2 d = v2(P.max_dist, -1.0f);
+    opu(d, sqrt_cr(m.l2) + m.k, m.id);
+    return d;
+}
+
 // One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
 // in flight while prim j is evaluated (A/B: +2% over loading at use). The IEEE sqrt sequence hipcc
 // is replaced by rmr::sqrt_cr (same bits, 6 fewer VALU per sqrt; rmr_math.h).

@@ -8,6 +8,7 @@
 // which the generated GLSL would not compile is reported as a SceneError instead.
 #include "scene.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -408,6 +409,13 @@ void CompiledScene::from_tables(const rmr_scene& s) {
     v2_slots = s.v2_n_slots;
     if (s.rm2) rm2 = *s.rm2; else std::memset(&rm2, 0, sizeof rm2);
     for (int i = 0; i < 3; i++) sky[i] = s.sky[i];
+}
+
+float max_sphere_radius(const CompiledScene& s) {
+    float r = 0.0f;
+    for (const rmr_prim& q : s.prims)
+        if (q.type == RMR_PRIM_SPHERE) r = std::max(r, std::fabs(q.r[0]));
+    return r;
 }
 
 double CompiledScene::flops_per_map() const {

@@ -33,5 +33,7 @@ struct CompiledScene {
 // GLSL would fail to compile.
 CompiledScene compile_scene(const std::string& json_text, int variant);
 CompiledScene builtin_scene(int variant);
+// largest |radius| of the scene's spheres (0 if none): the approximate-then-exact map's error scale
+float max_sphere_radius(const CompiledScene& s);
 
 }  // namespace rmr

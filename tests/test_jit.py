@@ -121,3 +121,45 @@ def test_jit_animated_scene_bitexact(renderer):
             assert (renderer.stats().jit_launches > 0) == (mode == 1)
         assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)), "frame %d" % frame
     renderer.set_jit(2)
+
+
+def _ties_scene():
+    """Cornell-5 plus exact and near duplicates: a second copy of the sphere with another material
+    (exact ties on its whole surface: the later object must win, RM1:219-222), a copy of the floor
+    shifted by one float ulp, and a sphere whose surface touches the left wall. These drive the
+    approximate-then-exact map (rmr_trace.h am_*) through its exact fallback on many lanes."""
+    import json
+    with open(os.path.join(SCENES, "cornell5.scene")) as f:
+        sc = json.load(f)
+    obj = sc["objects"]
+    dup = json.loads(json.dumps(obj[3]))
+    dup["matID"] = 1
+    obj.append(dup)
+    floor = json.loads(json.dumps(obj[0]))
+    floor["matID"] = 2
+    floor["nodes"][0]["inputs"][1][1] = float(np.nextafter(np.float32(-1.025), np.float32(0)))
+    obj.append(floor)
+    touch = json.loads(json.dumps(obj[3]))
+    touch["nodes"][0]["inputs"][1] = [-2.45, 1.0, 1.5]
+    touch["nodes"][0]["inputs"][2] = [0.5, 0.5, 0.5]
+    obj.append(touch)
+    return sc
+
+
+@pytest.mark.gpu
+def test_jit_approx_map_ties_bitexact(renderer):
+    sc = _ties_scene()
+    W, H = 48, 40
+    rect = (0, 0, W, H)
+    prm, view = _setup(renderer, sc, "rm1", W, H, {"max_bounces": 4})
+    renderer.set_jit(1)
+    try:
+        times = time_schedule(3, frame=2)
+        gpu = renderer.trace_samples(times, rect)
+        assert renderer.stats().jit_launches > 0
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(scene_compile.compile_scene(sc, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()

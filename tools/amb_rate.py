@@ -1,0 +1,30 @@
+"""Diagnostics: how often the approximate-then-exact map (rmr_trace.h am_*) falls back to the exact
+fold, per scene (RMR_JIT_AMBCOUNT=1 build of the JIT source; counters via rmr_get_section_cycles)."""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["RMR_JIT_AMBCOUNT"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
+from raymarchrenderer_amd._lib import lib  # noqa: E402
+
+G = os.path.join(ROOT, "tests", "golden", "scenes")
+r = Renderer(0, 1920, 1080)
+r.set_jit(1)
+for name, path, b in [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"), 4),
+                      ("multilight", os.path.join(G, "multilight.scene"), 16)]:
+    r.load_scene(path, "rm1")
+    r.set_params(abi.default_params(max_bounces=b))
+    r.reload()
+    r.reset_stats()
+    r.render_spp(time_schedule(4))
+    st = r.stats()
+    out = (C.c_uint64 * 4)()
+    lib().rmr_get_section_cycles(r._ctx, out)
+    print(json.dumps({"scene": name, "map_evals": st.map_evals, "map_iters": st.map_iters,
+                      "amb_lanes": out[0], "amb_waves": out[1],
+                      "amb_lane_frac": out[0] / max(1, st.map_evals), "amb_iter_frac": out[1] / max(1, st.map_iters)}))
+r.close()

@@ -1,0 +1,55 @@
+"""Same-process A/B of an environment switch read when the JIT source is generated
+(e.g. RMR_JIT_APPROX, RMR_JIT_BAKE, RMR_JIT_CULL): per scene, median trace time per setting and a
+bitwise comparison of the images.
+
+    python tools/env_ab.py RMR_JIT_APPROX 1 0 [--spp 16]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("var")
+ap.add_argument("values", nargs="+")
+ap.add_argument("--spp", type=int, default=16)
+ap.add_argument("--rounds", type=int, default=4)
+ap.add_argument("--scenes", default="", help="comma-separated subset of the scene names")
+a = ap.parse_args()
+
+G = os.path.join(ROOT, "tests", "golden", "scenes")
+CASES = [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"), "rm1", 4),
+         ("multilight", os.path.join(G, "multilight.scene"), "rm1", 16),
+         ("default", os.path.join(G, "default.scene"), "rm1", 16),
+         ("rm3", None, "rm3", 16)]
+r = Renderer(0, 1920, 1080)
+r.set_jit(1)
+times = time_schedule(a.spp)
+for name, path, variant, b in CASES:
+    if a.scenes and name not in a.scenes.split(","):
+        continue
+    res, img = {}, {}
+    for rnd in range(a.rounds + 1):
+        for v in a.values:
+            os.environ[a.var] = v
+            if path is None:
+                r.load_builtin(variant)
+            else:
+                r.load_scene(path, variant)
+            r.set_params(abi.default_params(max_bounces=b))
+            r.reload()
+            r.reset_stats()
+            r.render_spp(times)
+            st = r.stats()
+            if rnd:
+                res.setdefault(v, []).append(st.trace_ms)
+            img[v] = r.read_accum()
+    ref = img[a.values[0]].view(np.uint32)
+    print(json.dumps({"scene": name, **{"%s=%s_ms" % (a.var, k): round(float(np.median(t)), 2) for k, t in res.items()},
+                      "bitwise_equal": all(np.array_equal(ref, img[v].view(np.uint32)) for v in a.values)}), flush=True)
+r.close()
