@@ -153,6 +153,9 @@ int rmr_reset_stats(rmr_ctx* ctx);
  * cycles summed over all waves since rmr_reset_stats, split into [0] refill/ray setup, [1] map()
  * iterations, [2] shading batches, [3] whole trace loop. */
 int rmr_get_section_cycles(rmr_ctx* ctx, uint64_t out[4]);
+/* Raw kernel counters (diagnostics): [0] map evals, [1] map iterations, [2] shading batches,
+ * [4..7] the section cycles above (or the RMR_JIT_AMBCOUNT fallback counts, tools/amb_rate.py). */
+int rmr_get_counters(rmr_ctx* ctx, uint64_t out[16]);
 /* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */
 int rmr_set_kernel(rmr_ctx* ctx, int kernel);
 /* envTex of skyColor (RM1:78-113, RM2:84-107; the reference loads veranda_1k.hdr through SOIL as

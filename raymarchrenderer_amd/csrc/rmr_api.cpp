@@ -570,8 +570,8 @@ int rmr_create(rmr_ctx** out, int device) {
     c->own_stream = true;
     rmr_default_params(&c->params);
     if (hipMalloc((void**)&c->d_queue, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         rmr_destroy(c);
         return RMR_E_HIP;
     }
@@ -855,6 +855,16 @@ int rmr_get_section_cycles(rmr_ctx* c, uint64_t out[4]) {
     return RMR_OK;
 }
 
+int rmr_get_counters(rmr_ctx* c, uint64_t out[16]) {
+    if (!c || !out) return RMR_E_INVALID;
+    int r = rmr_sync(c);
+    if (r) return r;
+    unsigned long long cnt[16];
+    HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 16; i++) out[i] = cnt[i];
+    return RMR_OK;
+}
+
 int rmr_reset_stats(rmr_ctx* c) {
     if (!c) return RMR_E_INVALID;
     int r = rmr_sync(c);
@@ -862,7 +872,7 @@ int rmr_reset_stats(rmr_ctx* c) {
     const double fpm = c->stats.flops_per_map;
     c->stats = rmr_stats{};
     c->stats.flops_per_map = fpm;
-    HIPCHK(c, hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)));
     return RMR_OK;
 }
 

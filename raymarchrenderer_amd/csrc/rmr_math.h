@@ -75,6 +75,17 @@ RMR_D V3 mat_mul(V3 c0, V3 c1, V3 c2, V3 v) {
 RMR_D float clampf(float x, float a, float b) { return fminf(fmaxf(x, a), b); }
 RMR_D float fractf(float x) { return x - floorf(x); }
 RMR_D float modf_glsl(float x, float y) { return fmaf(-y, floorf(x / y), x); }
+// x / 3.14f (rand()'s mod(dt, 3.14), RM1:52) by two FMAs: q0 = x RN(1/3.14), one residual correction.
+// Bit-identical to the IEEE quotient for every finite |x| >= 2^-100 (all 2^32 inputs checked:
+// tools/probes/divconst_exhaustive.c); smaller, infinite and NaN inputs take the IEEE division.
+RMR_D float div_314(float x) {
+    const float y = 3.14f, rc = 0x1.461d58p-2f;
+    if (__builtin_expect(!(fabsf(x) >= 0x1p-100f) || fabsf(x) == __builtin_inff(), 0)) return x / y;
+    const float q0 = x * rc;
+    const float r = fmaf(-q0, y, x);
+    return fmaf(r, rc, q0);
+}
+RMR_D float mod_314(float x) { return fmaf(-3.14f, floorf(div_314(x)), x); }
 RMR_D V3 reflect(V3 I, V3 N) { float k = 2.0f * dot(N, I); return vfma(N, -k, I); }
 RMR_D V3 refract(V3 I, V3 N, float eta) {
     float d = dot(N, I);

@@ -92,7 +92,7 @@ RMR_D float rand_step(float gxt, float gyt, float& rc, V2 co) {
     co.x = fmaf(gxt, rc, co.x);
     co.y = fmaf(gyt, rc, co.y);
     float dt = dot2(co, v2(12.9898f, 78.233f));
-    float sn = modf_glsl(dt, 3.14f);
+    float sn = mod_314(dt);   // == modf_glsl(dt, 3.14f) bit for bit
     rc = fractf(det_sin(sn) * 43758.5453f);
     return rc;
 }
