@@ -80,6 +80,7 @@ struct rmr_ctx {
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
     int shade_threshold = 16;
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
+    int full_threshold = 48;    // nearest-primitive cache: lanes per full map() batch (BVH scenes; tuned on csg256)
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels)
@@ -456,6 +457,16 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.bvh = c->d_bvh; P.n_nodes = c->n_bvh; P.bvh_margin = c->bvh_margin;
     P.n_prims = (int)s.prims.size();
     P.am_r2 = 2.0f * rmr::max_sphere_radius(s);
+    {
+        float E = 0.0f;   // max |c|_inf + |r|_inf: scale of the float error of a box/sphere distance
+        for (const rmr_prim& q : s.prims) {
+            const float rr = q.type == RMR_PRIM_SPHERE ? std::fabs(q.r[0])
+                                                       : std::max({std::fabs(q.r[0]), std::fabs(q.r[1]), std::fabs(q.r[2])});
+            E = std::max(E, std::max({std::fabs(q.c[0]), std::fabs(q.c[1]), std::fabs(q.c[2])}) + rr);
+        }
+        P.npc_eps0 = E * 0x1p-17f + 0x1p-60f;
+    }
+    P.full_threshold = c->full_threshold;
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
     P.spec_sky = s.spectral_sky;
@@ -577,6 +588,8 @@ int rmr_create(rmr_ctx** out, int device) {
     }
     if (const char* e = std::getenv("RMR_SHADE_T")) c->shade_threshold = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RMR_REFILL_T")) c->refill_threshold = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RMR_FULL_T")) c->full_threshold = std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RMR_FULL_R")) c->full_threshold |= std::max(0, std::min(255, std::atoi(e))) << 8;
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }

@@ -74,6 +74,11 @@ struct Lane {
     uint32_t wl;   // RM3 hero wavelength
     float power;   // RM3
     int phase;
+    // nearest-primitive cache (MAP::kCache, see npc_* below): leaf-order index of the last exact
+    // minimiser, lower bound of every other primitive's distance minus the error terms (relative to
+    // the anchor point), and the anchor's ray parameter t
+    int cw;
+    float cs, cta;
 };
 template <bool HO> RMR_D V3& hitref(Lane& L) {
     if constexpr (HO) return L.o;
@@ -412,14 +417,94 @@ RMR_D V2 map_bvh(const KParams& P, V3 p) {
     return v2(dbest, jnan > jbest ? mnan : mbest);
 }
 
+// ---- nearest-primitive cache (exact culling over time; NP == -3) --------------------------------
+// A full map() at the anchor point p0 (map_bvh_npc) also returns its minimiser w (leaf-order index)
+// and s2, a lower bound of every other primitive's float distance at p0 (the second-smallest
+// evaluated distance, or a skipped node's box distance minus the culling margin). Box and sphere
+// SDFs are 1-Lipschitz, and the float evaluation F of either differs from the exact f by at most
+// eps(p) = 2^-17 (|p|_inf + E) (E = max |c|_inf + |r|_inf over the scene, 4x slack over the
+// rounding analysis; it also covers the rounding of p itself), so at any later point p at distance
+// <= delta from p0:  F_j(p) >= s2 - eps(p0) - delta - eps(p)  for every j != w.  When that exceeds
+// F_w(p) — evaluated exactly, one primitive — w is the unique minimiser and map(p) is
+// opU((maxDist, -1), F_w(p), id_w) by the fold's closed form (map_bvh): one primitive instead of a
+// BVH traversal. delta: along a ray (t - t0)(1 + 2^-21) (|d| <= 1 + 2^-22 for the normalized
+// directions of the HO kernels); getNormal probes h (1 + 2^-21) from the hit point; a bounce origin
+// hit +- N 0.003 (0.0031). NaN points always take the full map().
+RMR_D float npc_eps(const KParams& P, V3 p) {
+    const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
+    return fmaf(ax, 0x1p-17f, P.npc_eps0);
+}
+#define NPC_PROBE_DELTA 0.0010001f
+#define NPC_BOUNCE_DELTA 0.0031f
+// exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere: a sphere is
+// the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) = dot(v,v) for non-NaN v,
+// 0 + S = S) minus its radius; a box subtracts 0 (x - 0 = x). Per-lane index: vector loads.
+RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid) {
+    const float4* q = (const float4*)(P.dprims + k);
+    const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type mat_id
+    const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
+    const V3 c = v3(a.x, a.y, a.z);
+    const V3 h = box ? v3(a.w, b.x, b.y) : v3s(0.0f);
+    const float rad = box ? 0.0f : a.w;
+    mid = b.w;
+    const V3 qq = vabs(p - c) - h;
+    const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
+    return (k0 + length(vmax0(qq))) - rad;
+}
+// map_bvh plus the minimiser's leaf index kw (-1: none at or below maxDist, or a NaN) and s2
+RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2) {
+    typedef const __attribute__((address_space(4))) BvhNode CNode;
+    CNode* nodes = (CNode*)P.bvh;
+    CDPrim* pr = (CDPrim*)P.dprims;
+    float dbest = P.max_dist, mbest = -1.0f, mnan = -1.0f;
+    int jbest = -1, jnan = -1, kbest = -1;
+    float sec = __builtin_inff();
+    int i = 0;
+    while (i < P.n_nodes) {
+        const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
+        const V3 hi = v3(nodes[i].hi[0], nodes[i].hi[1], nodes[i].hi[2]);
+        const int count = nodes[i].count, skip = nodes[i].skip;
+        const V3 q = vmax0(vmax(lo - p, p - hi));
+        const float lb2 = dot(q, q);
+        const float t = fmaxf(dbest + fmaf(fabsf(dbest), 0x1p-18f, P.bvh_margin), P.bvh_margin);
+        const bool need = !(lb2 > t * t);   // NaN p: lb2 NaN -> needed
+        if (!__ballot(need)) {
+            // every primitive below is >= the node box distance - bvh_margin (map_bvh's culling rule)
+            sec = fminf(sec, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+            i = skip;
+            continue;
+        }
+        if (count == 0) { i++; continue; }
+        const int first = nodes[i].first;
+        for (int k = first; k < first + count; k++) {
+            const int tw = pr[k].type;
+            const int type = tw & 0xff, j = tw >> 8;
+            const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
+            const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
+            const float mid = pr[k].mat_id;
+            const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
+            sec = __builtin_amdgcn_fmed3f(dbest, dj, sec);   // second smallest (maxDist included: safe)
+            if (dj < dbest || (dj == dbest && j > jbest)) { dbest = dj; mbest = mid; jbest = j; kbest = k; }
+            if (dj != dj && j > jnan) { jnan = j; mnan = mid; }
+        }
+        i = skip;
+    }
+    kw = (jnan >= 0 || jbest < 0) ? -1 : kbest;
+    s2 = sec;
+    return v2(dbest, jnan > jbest ? mnan : mbest);
+}
+
 template <int NP>
 struct TableMap {
+    // NP == -3: the BVH map with the nearest-primitive cache (trace_main's kCache path)
+    static constexpr bool kCache = (NP == -3);
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
-        else if constexpr (NP == -2) return map_bvh(P, p);
+        else if constexpr (NP == -2 || NP == -3) return map_bvh(P, p);
         else return map_general(P, p);
     }
+    static RMR_D V2 full(const KParams& P, V3 p, int& kw, float& s2) { return map_bvh_npc(P, p, kw, s2); }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -578,6 +663,10 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
 template <int VAR, bool HO>
 RMR_D void next_bounce(const KParams& P, Lane& L) {
     if (L.bounces < P.max_bounces) {
+        // nearest-primitive cache: the new ray starts at t = 0 within NPC_BOUNCE_DELTA of the hit
+        // (HO kernels: hit +- N 0.003 / 0.002); harmless where the cache is off
+        L.cs -= NPC_BOUNCE_DELTA;
+        L.cta = 0.0f;
         L.bounces++;
         start_march<HO>(P, L, PH_MARCH);   // march sign = inside ? -1 : 1
     } else if (finish_trace<VAR, HO>(P, L)) {
@@ -598,6 +687,8 @@ RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
         return;
     }
     const V3 dir = primary_dir(P, px, py, time, rc);
+    L.cw = 0;
+    L.cs = -__builtin_inff();
     if (fresh) {
         L.unit = u;
         L.time = time;
@@ -637,6 +728,8 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
         L.phase = PH_IDLE;
         return;
     }
+    L.cw = 0;
+    L.cs = -__builtin_inff();
     L.unit = u;
     L.time = b.z;
     L.gxt = b.x;
@@ -655,7 +748,7 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
 // distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
-template <bool HO>
+template <bool HO, bool CACHE = false>
 RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
     const bool shadow = (L.phase == PH_SHADOW);
     const float dist = (L.inside && !shadow) ? -m.x : m.x;
@@ -663,6 +756,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         if (shadow) {          // sd = t; keep hit/mid/normal of the shaded point
             L.phase = PH_NEE;
         } else {
+            if constexpr (CACHE) L.cs -= (L.t - L.cta) * (1.0f + 0x1p-21f);   // cache now relative to the hit
             L.mid = m.y;
             hitref<HO>(L) = vfma(L.d, L.t, L.o);
             L.ctr = 0;
@@ -1096,7 +1190,7 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
-    uint64_t maps = 0, iters = 0, shades = 0;
+    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0;
     constexpr uint32_t CHUNK = 128;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
@@ -1171,7 +1265,49 @@ RMR_D void trace_main(const KParams& P) {
         RMR_STAMP(c1);
         const bool act = is_active(L.phase);
         const uint64_t amask = __ballot(act);
-        if (amask) {
+        if constexpr (MAP::kCache) {
+            if (amask) {
+                // nearest-primitive cache: one primitive where the bound holds; lanes where it does not
+                // wait for a full map() batch (>= full_threshold lanes, or no lane could use the cache)
+                V3 p = v3s(0.0f);
+                V2 m = v2(P.max_dist, -1.0f);
+                bool ok = false;
+                if (act) {
+                    p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
+                    float mid;
+                    const float F = prim_dist(P, L.cw, p, mid);
+                    const float delta = (L.phase == PH_NORMAL) ? NPC_PROBE_DELTA : (L.t - L.cta) * (1.0f + 0x1p-21f);
+                    const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
+                    ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > F);
+                    opu(m, F, mid);
+                }
+                const uint64_t okm = __ballot(act && ok);
+                const uint64_t fm = __ballot(act && !ok);
+                bool done = ok;
+                const int nf = __popcll(fm), nok = __popcll(okm);
+                const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
+                if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
+                    if (act && !ok) {
+                        int kw;
+                        float s2;
+                        m = MAP::full(P, p, kw, s2);
+                        L.cw = kw >= 0 ? kw : 0;
+                        L.cs = kw >= 0 ? s2 - npc_eps(P, p) - (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
+                                       : -__builtin_inff();
+                        L.cta = L.t;
+                        done = true;
+                    }
+                    fulls++;
+                }
+                if (done) {
+                    if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                    else march_update<HO, true>(P, L, m);
+                }
+                const uint64_t dm = __ballot(done);
+                maps += (uint64_t)__popcll(dm);
+                iters += dm ? 1 : 0;
+            }
+        } else if (amask) {
             if (act) {
                 const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
                 const V2 m = MAP::eval(P, p);
@@ -1203,6 +1339,7 @@ RMR_D void trace_main(const KParams& P) {
         atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
         atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
         atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
+        if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);

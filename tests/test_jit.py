@@ -163,3 +163,23 @@ def test_jit_approx_map_ties_bitexact(renderer):
     a, b = gpu[..., :3], cpu[..., :3]
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
+@pytest.mark.gpu
+def test_jit_bvh_nearest_primitive_cache_matches_table_kernel(renderer):
+    """csg256 (256 primitives, BVH map): the JIT kernel with the nearest-primitive cache (one
+    primitive per map() while the Lipschitz bound proves it the unique minimiser, rmr_trace.h npc_*)
+    equals the table-driven BVH kernel (no cache) bit for bit on a full render."""
+    W, H = 160, 120
+    _setup(renderer, os.path.join(SCENES, "csg256.scene"), "rm1", W, H, {"max_bounces": 4})
+    times = time_schedule(6, frame=3)
+    out = {}
+    for mode in (0, 1):
+        renderer.set_jit(mode)
+        renderer.reload()
+        renderer.reset_stats()
+        renderer.render_spp(times)
+        out[mode] = renderer.read_accum()
+        assert (renderer.stats().jit_launches > 0) == (mode == 1)
+    renderer.set_jit(2)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))

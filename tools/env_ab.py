@@ -18,6 +18,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("var")
 ap.add_argument("values", nargs="+")
 ap.add_argument("--spp", type=int, default=16)
+ap.add_argument("--W", type=int, default=1920)
+ap.add_argument("--H", type=int, default=1080)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--scenes", default="", help="comma-separated subset of the scene names")
 a = ap.parse_args()
@@ -26,8 +28,9 @@ G = os.path.join(ROOT, "tests", "golden", "scenes")
 CASES = [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"), "rm1", 4),
          ("multilight", os.path.join(G, "multilight.scene"), "rm1", 16),
          ("default", os.path.join(G, "default.scene"), "rm1", 16),
-         ("rm3", None, "rm3", 16)]
-r = Renderer(0, 1920, 1080)
+         ("rm3", None, "rm3", 16),
+         ("csg256", os.path.join(ROOT, "scenes", "csg256.scene"), "rm1", 4)]
+r = Renderer(0, a.W, a.H)
 r.set_jit(1)
 times = time_schedule(a.spp)
 for name, path, variant, b in CASES:
