@@ -170,6 +170,16 @@ int rmr_set_env_map(rmr_ctx* ctx, const uint8_t* rgba8, int w, int h);
  * mode 0 = off, 1 = always (errors are returned), 2 = auto (default: launches of >= 2^20 units;
  * a failed compile falls back to the table-driven kernel). Env RMR_JIT overrides at rmr_create. */
 int rmr_set_jit(rmr_ctx* ctx, int mode);
+/* Exact work-skipping in the trace kernels (all results bit-identical; only the count of map()
+ * calls changes), default all on; env RMR_ESC=0 / RMR_NPC=0 / RMR_JIT_APPROX=0 clear a bit at
+ * rmr_create:
+ *   RMR_CULL_ESCAPE: a march past the exit of the inflated scene box ends as its miss
+ *   RMR_CULL_NPC:    nearest-primitive cache of the BVH map (scenes of > 32 spheres/boxes)
+ *   RMR_CULL_APPROX: approximate-then-exact map() of sphere/box scenes (one exact sqrt) */
+#define RMR_CULL_ESCAPE 1
+#define RMR_CULL_NPC 2
+#define RMR_CULL_APPROX 4
+int rmr_set_culling(rmr_ctx* ctx, int flags);
 /* Compile the specialised kernel of a scene without a GPU (json NULL = the variant's built-in
  * scene). On success `log` receives the code-object key, otherwise the compiler log. */
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);

@@ -105,3 +105,9 @@ class Stats(C.Structure):
     _fields_ = [("map_evals", C.c_uint64), ("samples", C.c_uint64), ("trace_launches", C.c_uint64),
                 ("trace_ms", C.c_double), ("fold_ms", C.c_double), ("flops_per_map", C.c_double),
                 ("map_iters", C.c_uint64), ("shade_batches", C.c_uint64), ("jit_launches", C.c_uint64)]
+
+# rmr_set_culling flags (rmr.h)
+CULL_ESCAPE = 1
+CULL_NPC = 2
+CULL_APPROX = 4
+CULL_ALL = CULL_ESCAPE | CULL_NPC | CULL_APPROX

@@ -81,6 +81,7 @@ struct rmr_ctx {
     int shade_threshold = 16;
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
     int full_threshold = 48;    // nearest-primitive cache: lanes per full map() batch (BVH scenes; tuned on csg256)
+    int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels)
@@ -214,8 +215,8 @@ int ensure_jit(rmr_ctx* c) {
     if (c->jit_ready) return RMR_OK;
     // animation: same structure as the last specialised scene, different numbers -> stop baking the
     // numbers for this context (one structure-only kernel instead of a compile per frame)
-    const std::string struct_src = rmr::jit_source(c->scene, c->has_prog, false);
-    const std::string baked_src = rmr::jit_source(c->scene, c->has_prog, true);
+    const std::string struct_src = rmr::jit_source(c->scene, c->has_prog, false, c->cull);
+    const std::string baked_src = rmr::jit_source(c->scene, c->has_prog, true, c->cull);
     if (struct_src != c->jit_struct_src) c->jit_bake = true;                        // new layout
     else if (baked_src != c->jit_baked_src && !c->jit_baked_src.empty()) c->jit_bake = false;  // moved
     c->jit_struct_src = struct_src;
@@ -467,6 +468,30 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         P.npc_eps0 = E * 0x1p-17f + 0x1p-60f;
     }
     P.full_threshold = c->full_threshold;
+    {
+        // escape bound (rmr_trace.h ray_exit): scene box of a sphere/box scene inflated by 0.002 +
+        // 2^-16 (|eye| + 2E + 3 maxDist) >= 0.001 + 8 x the float error of a distance at any point a
+        // march reaches (|p| <= |eye| + E + 3 maxDist)
+        bool simple = !s.prims.empty();
+        double lo[3] = {1e30, 1e30, 1e30}, hi[3] = {-1e30, -1e30, -1e30}, E = 0.0;
+        for (const rmr_prim& q : s.prims) {
+            simple = simple && (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX);
+            for (int k = 0; k < 3; k++) {
+                const double h = std::fabs((double)(q.type == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]));
+                lo[k] = std::min(lo[k], (double)q.c[k] - h);
+                hi[k] = std::max(hi[k], (double)q.c[k] + h);
+                E = std::max(E, std::fabs((double)q.c[k]) + h);
+            }
+        }
+        double eye = 0.0;
+        for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));
+        const double infl = 0.002 + std::ldexp(eye + 2.0 * E + 3.0 * std::fabs((double)c->params.max_dist), -16);
+        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && std::isfinite(infl) ? 1 : 0;
+        for (int k = 0; k < 3; k++) {
+            P.esc_lo[k] = (float)(lo[k] - infl);
+            P.esc_hi[k] = (float)(hi[k] + infl);
+        }
+    }
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
     P.spec_sky = s.spectral_sky;
@@ -588,6 +613,9 @@ int rmr_create(rmr_ctx** out, int device) {
     }
     if (const char* e = std::getenv("RMR_SHADE_T")) c->shade_threshold = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RMR_REFILL_T")) c->refill_threshold = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
+    if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
+    if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
     if (const char* e = std::getenv("RMR_FULL_T")) c->full_threshold = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RMR_FULL_R")) c->full_threshold |= std::max(0, std::min(255, std::atoi(e))) << 8;
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
@@ -919,6 +947,13 @@ int rmr_set_jit(rmr_ctx* c, int mode) {
     if (!c || mode < 0 || mode > 2) return RMR_E_INVALID;
     c->jit_mode = mode;
     c->jit_failed = false;
+    return RMR_OK;
+}
+
+int rmr_set_culling(rmr_ctx* c, int flags) {
+    if (!c || (flags & ~(RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX))) return RMR_E_INVALID;
+    if (flags != c->cull) c->jit_ready = false;   // the specialised kernel depends on it
+    c->cull = flags;
     return RMR_OK;
 }
 

@@ -79,6 +79,7 @@ struct Lane {
     // the anchor point), and the anchor's ray parameter t
     int cw;
     float cs, cta;
+    float texit;   // escape bound of the current ray (ray_exit)
 };
 template <bool HO> RMR_D V3& hitref(Lane& L) {
     if constexpr (HO) return L.o;
@@ -429,7 +430,9 @@ RMR_D V2 map_bvh(const KParams& P, V3 p) {
 // opU((maxDist, -1), F_w(p), id_w) by the fold's closed form (map_bvh): one primitive instead of a
 // BVH traversal. delta: along a ray (t - t0)(1 + 2^-21) (|d| <= 1 + 2^-22 for the normalized
 // directions of the HO kernels); getNormal probes h (1 + 2^-21) from the hit point; a bounce origin
-// hit +- N 0.003 (0.0031). NaN points always take the full map().
+// hit +- N 0.003 (0.0031). NaN points always take the full map(). The cached bound also drops
+// |s2| 2^-20 for the rounding of the check's subtractions (bounded by s2, delta and eps, each
+// covered by that term or eps's slack).
 RMR_D float npc_eps(const KParams& P, V3 p) {
     const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
     return fmaf(ax, 0x1p-17f, P.npc_eps0);
@@ -545,11 +548,34 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
     return v3(top.x * ib + bot.x * b, top.y * ib + bot.y * b, top.z * ib + bot.z * b);
 }
 
+// Escape bound (HO kernels of sphere/box scenes, P.esc_on): esc_lo/esc_hi is the scene's bounding
+// box inflated by esc_infl >= 0.001 + the float error of any distance at any reachable point
+// (host: upload_scene). Once the ray is past the exit of that box no later march point can be
+// within 0.001 of a primitive, so march() can only end in its miss (t = maxDist, the same state
+// whichever step gets there): texit is an upper bound of the exit parameter, and a march whose t
+// passes it ends as a miss at once. The reference marches on to t >= maxDist (up to maxSteps) with
+// the same outcome; only the number of map() calls differs.
+RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
+    if (!P.esc_on) return __builtin_inff();
+    // per axis: (far plane - o) / d with v_rcp (1 ulp); the far plane follows the reciprocal's sign
+    // (d = -0 -> -inf -> the low plane); d == +-0 -> +-inf (no constraint / never inside);
+    // 0 * inf and NaN directions give NaN, which fminf drops (conservative)
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
+    const float tx = ((ix >= 0.0f ? P.esc_hi[0] : P.esc_lo[0]) - o.x) * ix;
+    const float ty = ((iy >= 0.0f ? P.esc_hi[1] : P.esc_lo[1]) - o.y) * iy;
+    const float tz = ((iz >= 0.0f ? P.esc_hi[2] : P.esc_lo[2]) - o.z) * iz;
+    const float te = fminf(tx, fminf(ty, tz));
+    // relative error of each quotient < 2^-21: widen positive bounds; a negative one means o is
+    // already outside and leaving on that axis
+    return te > 0.0f ? fmaf(te, 1.0f + 0x1p-19f, 0x1p-60f) : te;
+}
+
 template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
     L.t = 0.0f;
     L.ctr = 0;
-    if (P.max_steps > 0) {
+    if (HO && phase_on_run == PH_MARCH) L.texit = ray_exit(P, L.o, L.d);
+    if (P.max_steps > 0 && !(HO && phase_on_run == PH_MARCH && L.texit < 0.0f)) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
         L.t = P.max_dist;
@@ -769,6 +795,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         L.t = fmaf(dist, P.step_mult, L.t);
         L.ctr++;
         miss = (L.ctr >= P.max_steps);
+        if (HO && !shadow) miss = miss || L.t > L.texit;   // escaped (ray_exit)
     }
     if (miss) {
         L.t = P.max_dist;
@@ -1292,7 +1319,9 @@ RMR_D void trace_main(const KParams& P) {
                         float s2;
                         m = MAP::full(P, p, kw, s2);
                         L.cw = kw >= 0 ? kw : 0;
-                        L.cs = kw >= 0 ? s2 - npc_eps(P, p) - (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
+                        // |s2| 2^-20: the rounding of the check's own subtractions
+                        L.cs = kw >= 0 ? s2 - fmaf(fabsf(s2), 0x1p-20f, npc_eps(P, p)) -
+                                             (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
                                        : -__builtin_inff();
                         L.cta = L.t;
                         done = true;

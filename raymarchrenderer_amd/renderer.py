@@ -166,6 +166,10 @@ class Renderer:
         """hipRTC per-scene kernel specialisation: 0 off, 1 always, 2 auto (large launches)."""
         _check(self._ctx, lib().rmr_set_jit(self._ctx, int(mode)))
 
+    def set_culling(self, flags):
+        """Exact work-skipping switches (abi.CULL_*; results are bit-identical either way)."""
+        _check(self._ctx, lib().rmr_set_culling(self._ctx, int(flags)))
+
     def set_stream(self, hip_stream_handle):
         _check(self._ctx, lib().rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
 

@@ -177,8 +177,24 @@ def test_stats_count_map_evals(renderer):
     st = renderer.stats()
     orc = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H)
     orc.render(times)
-    # the kernels evaluate getNormal once per hit (the reference calls it per material node); the
-    # oracle does the same, so the counts agree exactly
-    assert st.map_evals == orc.map_evals
+    # the kernels evaluate getNormal once per hit (the reference calls it per material node), as the
+    # oracle does; on sphere/box scenes a march past the escape bound (rmr_trace.h ray_exit) ends
+    # as its miss without the remaining map() calls, so the kernels count fewer
+    assert 0.5 * orc.map_evals < st.map_evals <= orc.map_evals
     assert st.flops_per_map == 106
     assert st.trace_ms > 0
+
+
+@pytest.mark.gpu
+def test_stats_count_map_evals_exact_without_escape_bound(renderer):
+    """Node-program scenes march every step (no escape bound): the count equals the oracle's."""
+    W, H = 24, 24
+    path = os.path.join(GOLDEN, "scenes", "glass_test.scene")
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 4})
+    renderer.reset_stats()
+    times = time_schedule(2)
+    renderer.render_spp(times)
+    st = renderer.stats()
+    orc = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H)
+    orc.render(times)
+    assert st.map_evals == orc.map_evals

@@ -183,3 +183,32 @@ def test_jit_bvh_nearest_primitive_cache_matches_table_kernel(renderer):
         assert (renderer.stats().jit_launches > 0) == (mode == 1)
     renderer.set_jit(2)
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4)])
+def test_culling_switches_bitexact(renderer, scene, bounces, spp):
+    """The exact work-skipping paths (escape bound, nearest-primitive cache, approximate-then-exact
+    map; rmr_set_culling) change only the number of map() calls: full renders with every switch
+    on and with every switch off are bitwise equal, on the JIT and on the table-driven kernels."""
+    W, H = 192, 128
+    _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": bounces})
+    times = time_schedule(spp, frame=5)
+    out, evals = {}, {}
+    try:
+        for jit in (1, 0):
+            renderer.set_jit(jit)
+            for flags in (abi.CULL_ALL, 0):
+                renderer.set_culling(flags)
+                renderer.reload()
+                renderer.reset_stats()
+                renderer.render_spp(times)
+                out[(jit, flags)] = renderer.read_accum()
+                evals[(jit, flags)] = renderer.stats().map_evals
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+        renderer.set_jit(2)
+    ref = out[(0, 0)].view(np.uint32)
+    for k, img in out.items():
+        assert np.array_equal(ref, img.view(np.uint32)), k
+    assert evals[(1, abi.CULL_ALL)] < evals[(1, 0)] == evals[(0, 0)]

@@ -49,7 +49,9 @@ def main():
     args = ap.parse_args()
     text = open(args.scene).read().encode() if args.scene != "builtin" else b""
     ctxs = []
-    for p in args.libs:
+    for spec in args.libs:
+        # "path.so" or "path.so:FLAGS" (rmr_set_culling flags for this context)
+        p, _, cf = spec.partition(":")
         L = load(p)
         h = C.c_void_p()
         assert L.rmr_create(C.byref(h), 0) == 0
@@ -63,7 +65,10 @@ def main():
         L.rmr_set_params(h, C.byref(prm))
         if args.T:
             L.rmr_set_tuning(h, args.T, -1, 0)
-        ctxs.append((p, L, h))
+        if cf:
+            L.rmr_set_culling.argtypes = [C.c_void_p, C.c_int]
+            assert L.rmr_set_culling(h, int(cf)) == 0
+        ctxs.append((spec, L, h))
     times = time_schedule(args.spp)
     tp = times.ctypes.data_as(C.POINTER(C.c_float))
     res = {p: [] for p, _, _ in ctxs}

@@ -1,8 +1,9 @@
 """Same-process A/B of an environment switch read when the JIT source is generated
-(e.g. RMR_JIT_APPROX, RMR_JIT_BAKE, RMR_JIT_CULL): per scene, median trace time per setting and a
-bitwise comparison of the images.
+(e.g. RMR_JIT_BAKE, RMR_JIT_CULL), or of rmr_set_culling flags (var "culling"): per scene, median
+trace time per setting and a bitwise comparison of the images.
 
-    python tools/env_ab.py RMR_JIT_APPROX 1 0 [--spp 16]
+    python tools/env_ab.py culling 7 0 [--spp 16]
+    python tools/env_ab.py RMR_JIT_BAKE 1 0
 """
 import argparse
 import json
@@ -39,7 +40,10 @@ for name, path, variant, b in CASES:
     res, img = {}, {}
     for rnd in range(a.rounds + 1):
         for v in a.values:
-            os.environ[a.var] = v
+            if a.var == "culling":
+                r.set_culling(int(v))
+            else:
+                os.environ[a.var] = v
             if path is None:
                 r.load_builtin(variant)
             else:
