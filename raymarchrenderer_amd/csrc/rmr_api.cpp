@@ -56,6 +56,13 @@ struct rmr_ctx {
     rmr::DPrim* d_dprims = nullptr;
     rmr::DMat* d_dmats = nullptr;
     rmr::BvhNode* d_bvh = nullptr;
+    // escape bound (rmr_trace.h ray_exit): <= kMaxEscBoxes boxes covering every primitive (lo.xyz,
+    // hi.xyz), uploaded inflated by esc_infl (which depends on the view and maxDist)
+    std::vector<float> esc_raw;
+    std::vector<rmr::BvhNode> bvh_host;   // host copy of the BVH (escape-box cut)
+    std::vector<int> bvh_order;           // leaf-order -> scene index
+    float* d_esc = nullptr;
+    double esc_infl_dev = -1.0;
     float4* d_env = nullptr;              // envTex (rmr_set_env_map)
     int env_w = 0, env_h = 0;
     int n_bvh = 0;
@@ -146,6 +153,67 @@ constexpr size_t kMaxLoopPrims = 32;
 
 int upload_bvh(rmr_ctx* c);
 
+// Escape boxes: each primitive's box for scenes of <= kMaxEscBoxes primitives; for BVH scenes a cut
+// of the hierarchy (the always-visited large primitives individually, then the node with the most
+// primitives split until kMaxEscBoxes boxes). Their union covers every primitive.
+constexpr size_t kMaxEscBoxes = 32;
+void build_escape_boxes(rmr_ctx* c, bool simple) {
+    const CompiledScene& s = c->scene;
+    c->esc_raw.clear();
+    if (!simple || s.prims.empty()) return;
+    auto prim_box = [&](const rmr_prim& q, float* b) {
+        for (int k = 0; k < 3; k++) {
+            const float h = std::fabs(q.type == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]);
+            b[k] = q.c[k] - h;
+            b[3 + k] = q.c[k] + h;
+        }
+    };
+    float b[6];
+    if (c->map_np != -2) {
+        for (const rmr_prim& q : s.prims) {
+            prim_box(q, b);
+            c->esc_raw.insert(c->esc_raw.end(), b, b + 6);
+        }
+        return;
+    }
+    // BVH scene: nodes are in pre-order (first child = next node, second child = that node's skip);
+    // leaves of the always-visited list have infinite bounds: use their primitives' own boxes
+    std::vector<int> cut;
+    for (size_t i = 0; i < c->bvh_host.size();) {
+        const rmr::BvhNode& nd = c->bvh_host[i];
+        if (nd.lo[0] <= -1e38f) {   // always-visited leaf of large primitives
+            for (int k = nd.first; k < nd.first + nd.count; k++) {
+                prim_box(s.prims[(size_t)(c->bvh_order[(size_t)k])], b);
+                c->esc_raw.insert(c->esc_raw.end(), b, b + 6);
+            }
+            i = (size_t)nd.skip;
+            continue;
+        }
+        cut.push_back((int)i);   // root of the remaining hierarchy
+        break;
+    }
+    while (!cut.empty() && c->esc_raw.size() / 6 + cut.size() < kMaxEscBoxes) {
+        // split the internal node of the cut with the largest box
+        int best = -1;
+        float bestv = -1.0f;
+        for (size_t q = 0; q < cut.size(); q++) {
+            const rmr::BvhNode& nd = c->bvh_host[(size_t)cut[q]];
+            if (nd.count != 0) continue;
+            const float v = (nd.hi[0] - nd.lo[0]) * (nd.hi[1] - nd.lo[1]) * (nd.hi[2] - nd.lo[2]);
+            if (v > bestv) { bestv = v; best = (int)q; }
+        }
+        if (best < 0) break;
+        const int i = cut[(size_t)best];
+        cut[(size_t)best] = i + 1;
+        cut.push_back(c->bvh_host[(size_t)(i + 1)].skip);
+    }
+    for (int i : cut) {
+        const rmr::BvhNode& nd = c->bvh_host[(size_t)i];
+        for (int k = 0; k < 3; k++) { b[k] = nd.lo[k]; b[3 + k] = nd.hi[k]; }
+        c->esc_raw.insert(c->esc_raw.end(), b, b + 6);
+    }
+}
+
 int upload_scene(rmr_ctx* c) {
     const CompiledScene& s = c->scene;
     int r;
@@ -177,6 +245,8 @@ int upload_scene(rmr_ctx* c) {
         if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
         c->n_bvh = 0;
     }
+    build_escape_boxes(c, simple);
+    c->esc_infl_dev = -1.0;
     // shading kinds (RM1): recognise the single-node diffuse / emission materials
     std::vector<rmr::DMat> dm(std::max<size_t>(1, s.materials.size()));
     for (size_t i = 0; i < s.materials.size(); i++) {
@@ -341,6 +411,8 @@ int upload_bvh(rmr_ctx* c) {
     int r;
     if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
     if ((r = dev_upload(c, &c->d_bvh, nodes.data(), nodes.size()))) return r;
+    c->bvh_host = nodes;
+    c->bvh_order = order;
     c->n_bvh = (int)nodes.size();
     c->bvh_margin = 1e-4f + extent * 0x1p-16f;
     return RMR_OK;
@@ -469,28 +541,32 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     }
     P.full_threshold = c->full_threshold;
     {
-        // escape bound (rmr_trace.h ray_exit): scene box of a sphere/box scene inflated by 0.002 +
-        // 2^-16 (|eye| + 2E + 3 maxDist) >= 0.001 + 8 x the float error of a distance at any point a
-        // march reaches (|p| <= |eye| + E + 3 maxDist)
+        // escape bound (rmr_trace.h ray_exit): the escape boxes inflated by 0.002 + 2^-16 (|eye| + 2E +
+        // 3 maxDist) >= 0.001 + 8 x the float error of a distance at any point a march reaches
+        // (|p| <= |eye| + E + 3 maxDist) + the rounding of the slab parameters
         bool simple = !s.prims.empty();
-        double lo[3] = {1e30, 1e30, 1e30}, hi[3] = {-1e30, -1e30, -1e30}, E = 0.0;
+        double E = 0.0;
         for (const rmr_prim& q : s.prims) {
             simple = simple && (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX);
             for (int k = 0; k < 3; k++) {
                 const double h = std::fabs((double)(q.type == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]));
-                lo[k] = std::min(lo[k], (double)q.c[k] - h);
-                hi[k] = std::max(hi[k], (double)q.c[k] + h);
                 E = std::max(E, std::fabs((double)q.c[k]) + h);
             }
         }
         double eye = 0.0;
         for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));
         const double infl = 0.002 + std::ldexp(eye + 2.0 * E + 3.0 * std::fabs((double)c->params.max_dist), -16);
-        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && std::isfinite(infl) ? 1 : 0;
-        for (int k = 0; k < 3; k++) {
-            P.esc_lo[k] = (float)(lo[k] - infl);
-            P.esc_hi[k] = (float)(hi[k] + infl);
+        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && std::isfinite(infl) && !c->esc_raw.empty() ? 1 : 0;
+        if (P.esc_on && infl != c->esc_infl_dev) {
+            std::vector<float> bx(c->esc_raw.size());
+            for (size_t i = 0; i < bx.size(); i++)   // outward in double, then to float
+                bx[i] = (float)((double)c->esc_raw[i] + ((i % 6) < 3 ? -infl : infl));
+            int rr;
+            if ((rr = dev_upload(c, &c->d_esc, bx.data(), bx.size()))) return rr;
+            c->esc_infl_dev = infl;
         }
+        P.esc_boxes = c->d_esc;
+        P.n_esc = (int)(c->esc_raw.size() / 6);
     }
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
@@ -631,7 +707,7 @@ void rmr_destroy(rmr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
-    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_env, c->d_samp,
+    void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_esc, c->d_env, c->d_samp,
                     c->d_tiles, c->d_times, c->d_queue, c->d_counters};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

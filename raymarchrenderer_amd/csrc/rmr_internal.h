@@ -62,7 +62,8 @@ struct KParams {
     float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     float npc_eps0;             // nearest-primitive cache: 2^-17 E + 2^-60 (rmr_trace.h npc_eps)
     int32_t esc_on;             // escape bound (rmr_trace.h ray_exit): sphere/box scenes
-    float esc_lo[3], esc_hi[3]; // inflated scene bounding box
+    const float* esc_boxes;     // n_esc inflated boxes (lo.xyz, hi.xyz) covering every primitive
+    int32_t n_esc;
     int32_t full_threshold;     // nearest-primitive cache: bits 0-7 lanes per full map() batch; bits 8-15 R:
                                 // also a batch once waiting lanes x R >= 8 x cache-served lanes
     int32_t n_prims;

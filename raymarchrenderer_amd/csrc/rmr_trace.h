@@ -548,26 +548,36 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
     return v3(top.x * ib + bot.x * b, top.y * ib + bot.y * b, top.z * ib + bot.z * b);
 }
 
-// Escape bound (HO kernels of sphere/box scenes, P.esc_on): esc_lo/esc_hi is the scene's bounding
-// box inflated by esc_infl >= 0.001 + the float error of any distance at any reachable point
-// (host: upload_scene). Once the ray is past the exit of that box no later march point can be
-// within 0.001 of a primitive, so march() can only end in its miss (t = maxDist, the same state
-// whichever step gets there): texit is an upper bound of the exit parameter, and a march whose t
-// passes it ends as a miss at once. The reference marches on to t >= maxDist (up to maxSteps) with
-// the same outcome; only the number of map() calls differs.
+// Escape bound (HO kernels of sphere/box scenes, P.esc_on). esc_boxes are boxes whose union covers
+// every primitive, each inflated by >= 0.001 + the float error of any distance at any point a march
+// reaches + the rounding of the slab parameters below (host: launch setup; 0.002 + 2^-16 (|eye| +
+// 2E + 3 maxDist)). ray_exit returns an upper bound of the last ray parameter at which the ray is
+// inside any of them (-inf when it meets none ahead). Past it no march point can be within 0.001 of
+// a primitive, so march() can only end in its miss (t = maxDist, the same state whichever step gets
+// there): a march whose t passes texit ends as that miss at once. The reference marches on to
+// t >= maxDist (up to maxSteps) with the same outcome; only the number of map() calls differs.
+// Slab parameters use v_rcp (1 ulp): relative error < 2^-21, i.e. < 2^-21 x 3000 in space, far
+// inside the inflation slack; d == +-0 gives +-inf (no constraint / never inside); 0 x inf = NaN,
+// which the NaN-dropping fminf/fmaxf ignore (the ray then lies on a box face: >= the inflation
+// from every primitive). A NaN origin or direction (e.g. randHemisphere about a normal of exactly
+// (0,-1,0)) never escapes: the reference's map(NaN) "hits" at t = 0 (opU NaN rule).
 RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
-    if (!P.esc_on) return __builtin_inff();
-    // per axis: (far plane - o) / d with v_rcp (1 ulp); the far plane follows the reciprocal's sign
-    // (d = -0 -> -inf -> the low plane); d == +-0 -> +-inf (no constraint / never inside);
-    // 0 * inf and NaN directions give NaN, which fminf drops (conservative)
+    const float chk = ((o.x + o.y) + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
+    if (!P.esc_on || !(chk == chk)) return __builtin_inff();
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
-    const float tx = ((ix >= 0.0f ? P.esc_hi[0] : P.esc_lo[0]) - o.x) * ix;
-    const float ty = ((iy >= 0.0f ? P.esc_hi[1] : P.esc_lo[1]) - o.y) * iy;
-    const float tz = ((iz >= 0.0f ? P.esc_hi[2] : P.esc_lo[2]) - o.z) * iz;
-    const float te = fminf(tx, fminf(ty, tz));
-    // relative error of each quotient < 2^-21: widen positive bounds; a negative one means o is
-    // already outside and leaving on that axis
-    return te > 0.0f ? fmaf(te, 1.0f + 0x1p-19f, 0x1p-60f) : te;
+    float last = -__builtin_inff();
+    for (int b = 0; b < P.n_esc; b++) {
+        const float* B = P.esc_boxes + 6 * b;   // wave-uniform: scalar loads
+        const float ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
+        const float ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
+        const float az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
+        const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        // inside this box for t in [tn, tf] (nonempty and ahead): the ray may still hit its primitives
+        if (!(tn > tf)) last = fmaxf(last, tf);
+    }
+    // relative error < 2^-21: widen a positive bound
+    return last > 0.0f ? fmaf(last, 1.0f + 0x1p-19f, 0x1p-60f) : last;
 }
 
 template <bool HO>

@@ -185,14 +185,43 @@ def test_jit_bvh_nearest_primitive_cache_matches_table_kernel(renderer):
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
+def _shelf_scene():
+    """Cornell-5 plus a diffuse shelf under the light: rays bouncing up from the floor hit its bottom
+    face, whose getNormal is exactly (0,-1,0), where randHemisphere's frame is NaN (RM1:270-304) —
+    NaN directions, which the reference's march turns into a t = 0 hit (opU NaN rule)."""
+    import json
+    with open(os.path.join(SCENES, "cornell5.scene")) as f:
+        sc = json.load(f)
+    shelf = json.loads(json.dumps(sc["objects"][0]))
+    shelf["nodes"][0]["inputs"][1] = [0.0, 2.5, 0.0]
+    shelf["nodes"][0]["inputs"][2] = [1.0, 0.05, 1.0]
+    sc["objects"].append(shelf)
+    return sc
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4)])
+def test_shelf_nan_directions_bitexact_vs_oracle(renderer):
+    sc = _shelf_scene()
+    W, H = 40, 32
+    rect = (0, 0, W, H)
+    prm, view = _setup(renderer, sc, "rm1", W, H, {"max_bounces": 4})
+    times = time_schedule(4, frame=2)
+    gpu = renderer.trace_samples(times, rect)
+    cpu = oracle.Oracle(scene_compile.compile_scene(sc, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12)])
 def test_culling_switches_bitexact(renderer, scene, bounces, spp):
     """The exact work-skipping paths (escape bound, nearest-primitive cache, approximate-then-exact
     map; rmr_set_culling) change only the number of map() calls: full renders with every switch
     on and with every switch off are bitwise equal, on the JIT and on the table-driven kernels."""
     W, H = 192, 128
-    _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": bounces})
+    path = _shelf_scene() if scene == "shelf" else os.path.join(SCENES, scene)
+    _setup(renderer, path, "rm1", W, H, {"max_bounces": bounces})
     times = time_schedule(spp, frame=5)
     out, evals = {}, {}
     try:
