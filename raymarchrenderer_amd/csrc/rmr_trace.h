@@ -1302,7 +1302,7 @@ RMR_D void trace_main(const KParams& P) {
         RMR_STAMP(c1);
         const bool act = is_active(L.phase);
         const uint64_t amask = __ballot(act);
-        if constexpr (MAP::kCache) {
+        if constexpr (MAP::kCache && HO) {   // HO kernels only: normalized directions, fixed bounce offsets
             if (amask) {
                 // nearest-primitive cache: one primitive where the bound holds; lanes where it does not
                 // wait for a full map() batch (>= full_threshold lanes, or no lane could use the cache)
