@@ -61,6 +61,16 @@ RMR_D float sqrt_cr(float x) {
     return s;
 #endif
 }
+// sqrt_cr without its tiny-input branch: equal to sqrtf() for x == +-0, x >= 2^-96, +inf and NaN
+// (the caller routes 0 < x < 2^-96 and x < 0 elsewhere)
+RMR_D float sqrt_cr_big(float x) {
+    const float s0 = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s0) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s0) + 1u);
+    const float rm = fmaf(-sm, s0, x), rp = fmaf(-sp, s0, x);
+    float s = (rm <= 0.0f) ? sm : s0;
+    return (rp > 0.0f) ? sp : s;
+}
 RMR_D float length(V3 a) { return sqrt_cr(dot(a, a)); }
 RMR_D V3 normalize(V3 a) { float inv = 1.0f / length(a); return a * inv; }
 RMR_D V3 vfma(V3 a, float s, V3 b) { return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z)); }

@@ -269,13 +269,6 @@ RMR_D void opu_sphere_culled(V2& d, V3 p, V3 c, float r, float mid) {
 struct AMin {
     float a, s2, l2, k, id;
 };
-RMR_D void am_init(AMin& m) {
-    m.a = __builtin_inff();
-    m.s2 = __builtin_inff();
-    m.l2 = 0.0f;
-    m.k = 0.0f;
-    m.id = -1.0f;
-}
 RMR_D void am_take(AMin& m, float a, float l2, float k, float id) {
     m.s2 = __builtin_amdgcn_fmed3f(m.a, a, m.s2);
     const bool t = a < m.a;
@@ -283,6 +276,26 @@ RMR_D void am_take(AMin& m, float a, float l2, float k, float id) {
     m.l2 = t ? l2 : m.l2;
     m.k = t ? k : m.k;
     m.id = t ? id : m.id;
+}
+// the fold's first primitive initialises the state (a NaN there keeps a NaN, which am_unique rejects)
+RMR_D void am_first(AMin& m, float a, float l2, float k, float id) {
+    m.a = a;
+    m.s2 = __builtin_inff();
+    m.l2 = l2;
+    m.k = k;
+    m.id = id;
+}
+RMR_D void am_box0(AMin& m, V3 p, V3 c, V3 r, float id) {
+    const V3 q = vabs(p - c) - r;
+    const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
+    const V3 o = vmax0(q);
+    const float l2 = dot(o, o);
+    am_first(m, k + __builtin_amdgcn_sqrtf(l2), l2, k, id);
+}
+RMR_D void am_sphere0(AMin& m, V3 p, V3 c, float r, float id) {
+    const V3 v = p - c;
+    const float l2 = dot(v, v);
+    am_first(m, __builtin_amdgcn_sqrtf(l2) - r, l2, -r, id);
 }
 RMR_D void am_box(AMin& m, V3 p, V3 c, V3 r, float id) {
     const V3 q = vabs(p - c) - r;
@@ -296,16 +309,18 @@ RMR_D void am_sphere(AMin& m, V3 p, V3 c, float r, float id) {
     const float l2 = dot(v, v);
     am_take(m, __builtin_amdgcn_sqrtf(l2) - r, l2, -r, id);
 }
-// true when the minimiser is certain (see above); false for near ties, NaN and infinite values
+// true when the minimiser is certain (see above); false for near ties, NaN and infinite values, and
+// for a minimiser whose len2 is in sqrt_cr's tiny range (0 < len2 < 2^-96: the exact fold handles it)
 RMR_D bool am_unique(const AMin& m, float R2) {   // R2 = 2 R
     const float margin = fmaf(fabsf(m.a) + fabsf(m.s2) + R2, 0x1p-20f, 0x1p-39f);
-    return m.s2 - m.a > margin;
+    return m.s2 - m.a > margin && (m.l2 >= 0x1p-96f || m.l2 == 0.0f);
 }
 // exact result of a unique fold: opU((maxDist, -1), d_w, id_w); d_w = sqrt_cr(len2) + k is the same
-// expression as sd_box (k + length) and sd_sphere (length - r == length + (-r)).
+// expression as sd_box (k + length) and sd_sphere (length - r == length + (-r)). sqrt_cr_big: the
+// tiny range is excluded by am_unique (those lanes take the exact fold).
 RMR_D V2 am_result(const KParams& P, const AMin& m) {
     V2 d = v2(P.max_dist, -1.0f);
-    opu(d, sqrt_cr(m.l2) + m.k, m.id);
+    opu(d, sqrt_cr_big(m.l2) + m.k, m.id);
     return d;
 }
 
