@@ -595,11 +595,13 @@ RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
     return last > 0.0f ? fmaf(last, 1.0f + 0x1p-19f, 0x1p-60f) : last;
 }
 
+// te_pre: the ray's escape bound when the caller has it (primary rays: computed full-width with the
+// chunk's rays, chunk_ray); NaN = compute it here
 template <bool HO>
-RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
+RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
     L.t = 0.0f;
     L.ctr = 0;
-    if (HO && phase_on_run == PH_MARCH) L.texit = ray_exit(P, L.o, L.d);
+    if (HO && phase_on_run == PH_MARCH) L.texit = (te_pre == te_pre) ? te_pre : ray_exit(P, L.o, L.d);
     if (P.max_steps > 0 && !(HO && phase_on_run == PH_MARCH && L.texit < 0.0f)) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
@@ -616,7 +618,7 @@ RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run) {
 // trace() prologue: o = eye, d = dir, per-variant throughput init (RM1:485-492, RM2:422-429,
 // RM3:349-355). Returns false if the trace has zero bounces (loop body never runs).
 template <int VAR, bool HO>
-RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir) {
+RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir, float te_pre = __builtin_nanf("")) {
     L.o = v3(P.eye[0], P.eye[1], P.eye[2]);
     L.d = dir;
     L.bounces = 0;
@@ -626,7 +628,7 @@ RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir) {
     if (VAR == RMR_VARIANT_RM3) { L.wl = 0u; L.power = 1.0f; }
     if (L.bounces < P.max_bounces) {
         L.bounces = 1;
-        start_march<HO>(P, L, PH_MARCH);
+        start_march<HO>(P, L, PH_MARCH, te_pre);
         return true;
     }
     return false;
@@ -759,23 +761,29 @@ RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
 
 // Primary rays of a work chunk, computed full-width by the wave that fetches the chunk (instead of
 // by the few lanes each refill starts) and kept in LDS: (dir.xyz, randChange after the 3 jitter
-// rand() calls) and (gid.x + time, gid.y + time, time, in clip rect).
+// rand() calls) and (gid.x + time, gid.y + time, time, escape bound of the primary ray (HO kernels;
+// 1 otherwise) or NaN outside the clip rect).
 struct ChunkRay { float4 a, b; };
+template <bool HO>
 RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
     int px, py;
     float time, rc = 0.0f;
     ChunkRay r;
     const bool in_rect = unit_pixel(P, u, px, py, time);
     V3 dir = v3s(0.0f);
-    if (in_rect) dir = primary_dir(P, px, py, time, rc);
+    float te = __builtin_nanf("");
+    if (in_rect) {
+        dir = primary_dir(P, px, py, time, rc);
+        te = HO ? ray_exit(P, v3(P.eye[0], P.eye[1], P.eye[2]), dir) : 1.0f;   // never NaN
+    }
     r.a = make_float4(dir.x, dir.y, dir.z, rc);
-    r.b = make_float4((float)px + time, (float)py + time, time, in_rect ? 1.0f : 0.0f);
+    r.b = make_float4((float)px + time, (float)py + time, time, te);
     return r;
 }
 // begin_trace for a fresh unit whose primary ray is in LDS
 template <int VAR, bool HO>
 RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b) {
-    if (b.w == 0.0f) {
+    if (!(b.w == b.w)) {   // outside the clip rect
         L.phase = PH_IDLE;
         return;
     }
@@ -789,7 +797,7 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
     L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
     const V3 dir = v3(a.x, a.y, a.z);
     for (;;) {  // a zero-bounce trace finishes at once (and may start the next channel)
-        if (trace_prologue<VAR, HO>(P, L, dir)) return;
+        if (trace_prologue<VAR, HO>(P, L, dir, HO ? b.w : __builtin_nanf(""))) return;
         if (finish_trace<VAR, HO>(P, L)) {
             L.phase = PH_DONE;
             return;
@@ -1281,7 +1289,7 @@ RMR_D void trace_main(const KParams& P) {
                     if (!exhausted) {  // the chunk's primary rays, all 64 lanes at once
                         chunk_base = base;
                         for (uint32_t sl = __lane_id(); sl < CHUNK; sl += 64) {
-                            if (base + sl < rend) s_ray[wv][sl] = chunk_ray(P, base + sl);
+                            if (base + sl < rend) s_ray[wv][sl] = chunk_ray<HO>(P, base + sl);
                         }
                         __builtin_amdgcn_wave_barrier();
                     }
