@@ -157,13 +157,27 @@ int upload_bvh(rmr_ctx* c);
 // of the hierarchy (the always-visited large primitives individually, then the node with the most
 // primitives split until kMaxEscBoxes boxes). Their union covers every primitive.
 constexpr size_t kMaxEscBoxes = 32;
+// A Mandelbulb primitive (sd_mandelbulb) takes part when it iterates at least once with a bailout
+// >= 1.5: at |p - c| > bailout its loop stops at once with r = |p - c|, dr = 1, so its distance is
+// 0.5 log(r) r >= 0.30 — the box c +- bailout then bounds everything within 0.001 of it.
+bool escape_prim(const rmr_prim& q) {
+    if (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX) return true;
+    return q.type == RMR_PRIM_MANDELBULB && q.r[1] >= 1.0f && q.r[2] >= 1.5f && std::isfinite(q.r[2]);
+}
+float escape_halfwidth(const rmr_prim& q, int k) {
+    if (q.type == RMR_PRIM_SPHERE) return std::fabs(q.r[0]);
+    if (q.type == RMR_PRIM_MANDELBULB) return q.r[2];
+    return std::fabs(q.r[k]);
+}
 void build_escape_boxes(rmr_ctx* c, bool simple) {
     const CompiledScene& s = c->scene;
     c->esc_raw.clear();
-    if (!simple || s.prims.empty()) return;
+    bool ok = !s.prims.empty();
+    for (const rmr_prim& q : s.prims) ok = ok && escape_prim(q);
+    if (!ok || (!simple && s.prims.size() > kMaxEscBoxes)) return;
     auto prim_box = [&](const rmr_prim& q, float* b) {
         for (int k = 0; k < 3; k++) {
-            const float h = std::fabs(q.type == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]);
+            const float h = escape_halfwidth(q, k);
             b[k] = q.c[k] - h;
             b[3 + k] = q.c[k] + h;
         }
@@ -547,11 +561,9 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         bool simple = !s.prims.empty();
         double E = 0.0;
         for (const rmr_prim& q : s.prims) {
-            simple = simple && (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX);
-            for (int k = 0; k < 3; k++) {
-                const double h = std::fabs((double)(q.type == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]));
-                E = std::max(E, std::fabs((double)q.c[k]) + h);
-            }
+            simple = simple && escape_prim(q);
+            if (!escape_prim(q)) continue;
+            for (int k = 0; k < 3; k++) E = std::max(E, std::fabs((double)q.c[k]) + (double)escape_halfwidth(q, k));
         }
         double eye = 0.0;
         for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));

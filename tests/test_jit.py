@@ -214,7 +214,8 @@ def test_shelf_nan_directions_bitexact_vs_oracle(renderer):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12)])
+@pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12),
+                                               ("mandelbulb.scene", 2, 2)])
 def test_culling_switches_bitexact(renderer, scene, bounces, spp):
     """The exact work-skipping paths (escape bound, nearest-primitive cache, approximate-then-exact
     map; rmr_set_culling) change only the number of map() calls: full renders with every switch
