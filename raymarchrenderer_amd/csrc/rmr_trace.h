@@ -140,12 +140,20 @@ __device__ __noinline__ float sd_mandelbulb(V3 p, V3 c, V3 prm) {               
         if (r > bail) break;
         float theta = det_acos(z.z / r);
         float phi = det_atan2(z.y, z.x);
-        dr = fmaf(det_pow(r, power - 1.0f) * power, dr, 1.0f);
-        float zr = det_pow(r, power);
+        // det_pow(r, power - 1) and det_pow(r, power) with their shared det_log(r) computed once,
+        // and sin/cos of one angle from one reduction (det_sincos): the same operations as the
+        // separate calls, so the same bits
+        const float lr = (r == 0.0f) ? 0.0f : det_log(r);
+        const float pm1 = power - 1.0f;
+        const float pw1 = (pm1 == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(pm1 * lr));
+        dr = fmaf(pw1 * power, dr, 1.0f);
+        const float zr = (power == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(power * lr));
         theta = theta * power;
         phi = phi * power;
-        float st = det_sin(theta);
-        z = vfma(v3(st * det_cos(phi), det_sin(phi) * st, det_cos(theta)), zr, p0);
+        float st, ct, sph, cph;
+        det_sincos(theta, st, ct);
+        det_sincos(phi, sph, cph);
+        z = vfma(v3(st * cph, sph * st, ct), zr, p0);
     }
     return 0.5f * det_log(r) * r / dr;
 }
