@@ -1250,8 +1250,13 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 #define RMR_FAST_WAVES 8
 #endif
 // waves/SIMD the register allocator targets (launch bounds of the kernels that call trace_main)
+#ifndef RMR_GENERAL_WAVES
+#define RMR_GENERAL_WAVES 1
+#endif
 template <int VAR, bool GENERAL, bool PROG>
-constexpr int trace_waves() { return (GENERAL || PROG || VAR == RMR_VARIANT_RM2) ? 1 : RMR_FAST_WAVES; }
+constexpr int trace_waves() {
+    return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
+}
 
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
