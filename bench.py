@@ -15,7 +15,8 @@ The other BASELINE configs run with --config (they are separate bench lines, not
 
 Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL). The frame's 32x32 tiles
 are dealt round-robin to the ranks; each rank renders its tiles into a zeroed full-frame
-accumulator (x + 0 = x, so the reduce is exact). Total work is fixed => "scaling": "strong".
+accumulator (x + 0 = x, so the reduce is exact); frame f's reduce overlaps frame f + 1's render
+(two accumulators). Total work is fixed => "scaling": "strong".
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
@@ -125,8 +126,9 @@ def main():
     from raymarchrenderer_amd.multi_gpu import FrameRenderer
     stream = torch.cuda.current_stream()
     r.set_stream(stream.cuda_stream)
-    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-    fr = FrameRenderer(r, acc, W, H, TILE, rank, world, dist if dist_on else None)
+    # two accumulators when there is a reduce: frame f's reduce overlaps frame f + 1's render
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2 if dist_on else 1)]
+    fr = FrameRenderer(r, accs, W, H, TILE, rank, world, dist if dist_on else None)
     animated = bool(cfg.get("animated"))
     static_times = time_schedule(spp)
     frame_no = [0]
@@ -142,6 +144,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    fr.finish()
     torch.cuda.synchronize()
     r.reset_stats()
     if dist_on:
@@ -150,6 +153,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    fr.finish()   # every frame's reduce is inside the timed region
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()

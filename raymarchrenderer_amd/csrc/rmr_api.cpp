@@ -901,8 +901,11 @@ void* rmr_accum_device_ptr(rmr_ctx* c) { return c ? (void*)c->d_accum : nullptr;
 int rmr_bind_accum(rmr_ctx* c, void* ptr, size_t bytes) {
     if (!c || !ptr) return RMR_E_INVALID;
     if (bytes < (size_t)c->W * c->H * sizeof(float4)) return fail(c, RMR_E_INVALID, "bound accumulator too small");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
+    if (c->d_accum && !c->accum_external) {  // the context's own buffer: free it once idle
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_accum);
+    }
+    // (an external buffer is only swapped: launches already queued keep the pointer they captured)
     c->d_accum = (float4*)ptr;
     c->accum_external = true;
     return RMR_OK;

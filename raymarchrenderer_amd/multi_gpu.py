@@ -5,6 +5,10 @@ RGBA32F accumulator that is zero outside those tiles, then a single reduce(SUM) 
 rank 0 assembles the image. x + 0 = x, so the reduced image is bitwise the single-GPU image.
 Tiles are dealt round-robin in raster order, so every rank gets a spread of cheap (sky) and
 expensive (floor, walls) tiles.
+
+Frames are pipelined over two accumulators: frame f's reduce runs (async, on the collective's own
+stream) while frame f + 1 renders into the other buffer; a buffer is reused only after its reduce
+completed. The reduce of every frame is still one collective over the whole frame.
 """
 import numpy as np
 
@@ -19,25 +23,59 @@ def tile_partition(W, H, tile, rank, world):
     return np.array(t[rank::world], np.int32).reshape(-1, 2)
 
 
-def reduce_frame(accum, dist, group=None):
-    """Sum every rank's accumulator onto rank 0 (one collective per frame)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM, group=group)
-    return accum
+def _multi(dist, group=None):
+    return dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def reduce_frame(accum, dist, group=None, async_op=False):
+    """Sum every rank's accumulator onto rank 0 (one collective per frame). With async_op the
+    collective's work handle is returned (None without a collective)."""
+    if _multi(dist, group):
+        w = dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return w if async_op else accum
+    return None if async_op else accum
 
 
 class FrameRenderer:
-    """One rank's share of a frame: `renderer` renders into `accum` (a torch CUDA tensor of
-    H x W x 4 float32 bound with rmr_bind_accum), then the reduce."""
+    """One rank's share of each frame.
 
-    def __init__(self, renderer, accum, W, H, tile, rank, world, dist=None):
-        self.r, self.acc, self.dist = renderer, accum, dist
+    `accums`: one torch tensor (H x W x 4 float32) or a list of two for the pipelined schedule.
+    `renderer`: a raymarchrenderer_amd.Renderer (the accumulator is bound with rmr_bind_accum), or
+    None with `render_fn(acc, tiles, times, first_sample)` (tests: the CPU oracle under gloo)."""
+
+    def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None):
+        self.r, self.dist, self.render_fn = renderer, dist, render_fn
+        self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
+        self.work = [None] * len(self.accs)
         self.tiles = tile_partition(W, H, tile, rank, world)
         self.tile = tile
-        renderer.bind_accum(accum.data_ptr(), accum.numel() * accum.element_size())
+        self.f = 0
+        self.last = None
 
     def frame(self, times, first_sample=0):
-        self.acc.zero_()
+        """Render this rank's tiles of the next frame and start its reduce; returns the frame's
+        accumulator (complete on rank 0 once `finish()` or the next reuse of the buffer waited)."""
+        i = self.f % len(self.accs)
+        acc = self.accs[i]
+        if self.work[i] is not None:  # the reduce of the frame that last used this buffer
+            self.work[i].wait()
+            self.work[i] = None
+        acc.zero_()
         if len(self.tiles):
-            self.r.render_tiles(times, self.tiles, self.tile, first_sample=first_sample)
-        return reduce_frame(self.acc, self.dist)
+            if self.render_fn is not None:
+                self.render_fn(acc, self.tiles, times, first_sample)
+            else:
+                self.r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
+                self.r.render_tiles(times, self.tiles, self.tile, first_sample=first_sample)
+        self.work[i] = reduce_frame(acc, self.dist, async_op=True)
+        self.f += 1
+        self.last = acc
+        return acc
+
+    def finish(self):
+        """Wait for every outstanding reduce; returns the last frame's accumulator."""
+        for i, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[i] = None
+        return self.last

@@ -12,7 +12,7 @@ import torch.multiprocessing as mp
 
 from oracle import camera, oracle, scene_compile
 from raymarchrenderer_amd import abi, time_schedule
-from raymarchrenderer_amd.multi_gpu import frame_tiles, reduce_frame, tile_partition
+from raymarchrenderer_amd.multi_gpu import FrameRenderer, frame_tiles, reduce_frame, tile_partition
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W, H, TILE = 40, 24, 16
@@ -72,3 +72,41 @@ def test_gloo_two_ranks_reduce_is_exact():
         assert p.exitcode == 0
     want = _render_tiles(frame_tiles(W, H, TILE), time_schedule(2))
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def _oracle_into(acc, tiles, times, first_sample):
+    acc.copy_(torch.from_numpy(_render_tiles(tiles, times)))
+
+
+def _pipelined_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32) for _ in range(2)]
+    fr = FrameRenderer(None, accs, W, H, TILE, rank, world, dist, render_fn=_oracle_into)
+    for f in range(3):   # frame 2 reuses buffer 0 after waiting for frame 0's reduce
+        fr.frame(time_schedule(2, frame=f))
+    last = fr.finish()
+    if rank == 0:
+        q.put((last.numpy().copy(), accs[1].numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_ranks_pipelined_frames_exact():
+    """FrameRenderer's two-buffer schedule (async reduce of frame f while frame f + 1 renders):
+    every frame's reduced image equals the single-process render."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    f2, f1 = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for got, f in ((f2, 2), (f1, 1)):
+        want = _render_tiles(frame_tiles(W, H, TILE), time_schedule(2, frame=f))
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f
