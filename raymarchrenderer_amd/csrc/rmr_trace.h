@@ -465,26 +465,34 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 // exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere: a sphere is
 // the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) = dot(v,v) for non-NaN v,
 // 0 + S = S) minus its radius; a box subtracts 0 (x - 0 = x). Per-lane index: vector loads.
-RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid) {
+RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
     const float4* q = (const float4*)(P.dprims + k);
-    const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type mat_id
+    const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type|index<<8 mat_id
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
     const V3 c = v3(a.x, a.y, a.z);
     const V3 h = box ? v3(a.w, b.x, b.y) : v3s(0.0f);
     const float rad = box ? 0.0f : a.w;
     mid = b.w;
+    j = __float_as_int(b.z) >> 8;
     const V3 qq = vabs(p - c) - h;
     const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
     return (k0 + length(vmax0(qq))) - rad;
 }
-// map_bvh plus the minimiser's leaf index kw (-1: none at or below maxDist, or a NaN) and s2
-RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2) {
+// map_bvh plus the minimiser's leaf index kw (-1: none at or below maxDist, or a NaN) and s2.
+// Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id
+// ms; ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
+// distance tightens the culling bound from the first node on.
+RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2, int ks, int js, float ds, float ms) {
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
     CDPrim* pr = (CDPrim*)P.dprims;
     float dbest = P.max_dist, mbest = -1.0f, mnan = -1.0f;
     int jbest = -1, jnan = -1, kbest = -1;
     float sec = __builtin_inff();
+    if (ks >= 0) {   // (a NaN ds is never seeded: the caller passes ks = -1)
+        sec = __builtin_amdgcn_fmed3f(dbest, ds, sec);
+        if (ds <= dbest) { dbest = ds; mbest = ms; jbest = js; kbest = ks; }
+    }
     int i = 0;
     while (i < P.n_nodes) {
         const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
@@ -508,6 +516,7 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2) {
             const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
             const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
             const float mid = pr[k].mat_id;
+            if (k == ks) continue;   // the seed, already folded in
             const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
             sec = __builtin_amdgcn_fmed3f(dbest, dj, sec);   // second smallest (maxDist included: safe)
             if (dj < dbest || (dj == dbest && j > jbest)) { dbest = dj; mbest = mid; jbest = j; kbest = k; }
@@ -530,7 +539,9 @@ struct TableMap {
         else if constexpr (NP == -2 || NP == -3) return map_bvh(P, p);
         else return map_general(P, p);
     }
-    static RMR_D V2 full(const KParams& P, V3 p, int& kw, float& s2) { return map_bvh_npc(P, p, kw, s2); }
+    static RMR_D V2 full(const KParams& P, V3 p, int& kw, float& s2, int ks, int js, float ds, float ms) {
+        return map_bvh_npc(P, p, kw, s2, ks, js, ds, ms);
+    }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1345,10 +1356,11 @@ RMR_D void trace_main(const KParams& P) {
                 V3 p = v3s(0.0f);
                 V2 m = v2(P.max_dist, -1.0f);
                 bool ok = false;
+                float F = 0.0f, mid = -1.0f;
+                int jw = 0;
                 if (act) {
                     p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
-                    float mid;
-                    const float F = prim_dist(P, L.cw, p, mid);
+                    F = prim_dist(P, L.cw, p, mid, jw);
                     const float delta = (L.phase == PH_NORMAL) ? NPC_PROBE_DELTA : (L.t - L.cta) * (1.0f + 0x1p-21f);
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
                     ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > F);
@@ -1363,7 +1375,7 @@ RMR_D void trace_main(const KParams& P) {
                     if (act && !ok) {
                         int kw;
                         float s2;
-                        m = MAP::full(P, p, kw, s2);
+                        m = MAP::full(P, p, kw, s2, F == F ? L.cw : -1, jw, F, mid);
                         L.cw = kw >= 0 ? kw : 0;
                         // |s2| 2^-20: the rounding of the check's own subtractions
                         L.cs = kw >= 0 ? s2 - fmaf(fabsf(s2), 0x1p-20f, npc_eps(P, p)) -
