@@ -98,8 +98,8 @@ struct rmr_ctx {
     bool jit_failed = false;    // compile/load failed for the loaded scene (auto mode falls back)
     rmr::JitKernel jit;
     std::string jit_struct_src;  // structure-only source of the last specialised scene
-    std::string jit_baked_src;   // its baked source
-    bool jit_bake = true;        // false once a reload only moved primitives (animation)
+    std::vector<rmr_prim> jit_base;   // primitive values the specialised kernel was baked with
+    std::vector<char> jit_live;       // primitives that moved since: loaded, not literals
     std::vector<rmr::JitKernel> jit_loaded;  // modules loaded by this context (unloaded at destroy)
     size_t samp_budget = (size_t)8 << 30;
     std::string err;
@@ -297,15 +297,20 @@ int upload_scene(rmr_ctx* c) {
 // Compile (or fetch from the cache) and load the specialised trace kernel of the loaded scene.
 int ensure_jit(rmr_ctx* c) {
     if (c->jit_ready) return RMR_OK;
-    // animation: same structure as the last specialised scene, different numbers -> stop baking the
-    // numbers for this context (one structure-only kernel instead of a compile per frame)
+    // animation: same structure as the last specialised scene, different numbers -> the primitives
+    // that changed since the kernel's baked values become loads ("live"), the others stay literals:
+    // one compile when the motion starts, then the same kernel every frame
     const std::string struct_src = rmr::jit_source(c->scene, c->has_prog, false, c->cull);
-    const std::string baked_src = rmr::jit_source(c->scene, c->has_prog, true, c->cull);
-    if (struct_src != c->jit_struct_src) c->jit_bake = true;                        // new layout
-    else if (baked_src != c->jit_baked_src && !c->jit_baked_src.empty()) c->jit_bake = false;  // moved
+    const auto& prims = c->scene.prims;
+    if (struct_src != c->jit_struct_src || c->jit_base.size() != prims.size()) {   // new layout
+        c->jit_base = prims;
+        c->jit_live.assign(prims.size(), 0);
+    } else {
+        for (size_t j = 0; j < prims.size(); j++)
+            if (std::memcmp(&prims[j], &c->jit_base[j], sizeof(rmr_prim)) != 0) c->jit_live[j] = 1;
+    }
     c->jit_struct_src = struct_src;
-    c->jit_baked_src = baked_src;
-    const std::string& src = c->jit_bake ? baked_src : struct_src;
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live);
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {

@@ -28,8 +28,11 @@ struct JitKernel {
 // primitives' numbers are literals (fastest: +6-12% over loading them); otherwise only the scene's
 // structure is compiled and the numbers are scalar loads, so a scene that only moves (an animation)
 // reuses one kernel instead of recompiling per frame.
-// cull: RMR_CULL_* bits of the context (rmr.h): approximate-then-exact map, nearest-primitive cache
-std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7);
+// cull: RMR_CULL_* bits of the context (rmr.h): approximate-then-exact map, nearest-primitive cache.
+// live (with bake): primitives j with live[j] != 0 are loaded even so (an animation's moving
+// primitives; the rest stay literals).
+std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
+                       const std::vector<char>* live = nullptr);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);
