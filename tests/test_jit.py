@@ -215,14 +215,14 @@ def test_shelf_nan_directions_bitexact_vs_oracle(renderer):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12),
-                                               ("mandelbulb.scene", 2, 2)])
+                                               ("mandelbulb.scene", 2, 2), ("rm3", 16, 8)])
 def test_culling_switches_bitexact(renderer, scene, bounces, spp):
     """The exact work-skipping paths (escape bound, nearest-primitive cache, approximate-then-exact
     map; rmr_set_culling) change only the number of map() calls: full renders with every switch
     on and with every switch off are bitwise equal, on the JIT and on the table-driven kernels."""
     W, H = 192, 128
-    path = _shelf_scene() if scene == "shelf" else os.path.join(SCENES, scene)
-    _setup(renderer, path, "rm1", W, H, {"max_bounces": bounces})
+    path = _shelf_scene() if scene == "shelf" else (None if scene == "rm3" else os.path.join(SCENES, scene))
+    _setup(renderer, path, "rm3" if scene == "rm3" else "rm1", W, H, {"max_bounces": bounces})
     times = time_schedule(spp, frame=5)
     out, evals = {}, {}
     try:
