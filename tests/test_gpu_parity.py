@@ -42,6 +42,8 @@ CASES = [
     ("rm1_cornell5_steps0", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_steps": 0}),
     ("rm1_empty", os.path.join(SCENES, "empty.scene"), "rm1", {}),
     ("rm2_simple_sepch", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"separate_channels": 1}),
+    # separateChannels on the HO fast kernel (escape bound + approximate map per channel trace)
+    ("rm1_cornell5_sepch", os.path.join(SCENES, "cornell5.scene"), "rm1", {"separate_channels": 1, "max_bounces": 4}),
 ]
 
 
@@ -198,3 +200,28 @@ def test_stats_count_map_evals_exact_without_escape_bound(renderer):
     orc = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H)
     orc.render(times)
     assert st.map_evals == orc.map_evals
+
+
+@pytest.mark.parametrize("scene", ["cornell5.scene", "csg256.scene"])
+def test_far_camera_bitexact(renderer, scene):
+    """A camera 400 units away: larger escape-box inflation (|eye| term), long primary marches
+    through empty space, the nearest-primitive cache far from the scene."""
+    import math
+    W, H = 40, 30
+    path = os.path.join(SCENES, scene)
+    prm, _ = _setup(renderer, path, "rm1", W, H, {"max_bounces": 3})
+    eye = (30.0, 60.0, -400.0)
+    d = (-30.0, -59.0, 400.0)
+    m = math.sqrt(sum(x * x for x in d))
+    view = camera.view_uniforms(eye, tuple(x / m for x in d), W / H, camera.F(3.141592653) / camera.F(24))
+    renderer.set_view(view)
+    rect = (0, 0, W, H)
+    times = time_schedule(3, frame=4)
+    renderer.set_jit(1)
+    try:
+        gpu = renderer.trace_samples(times, rect)
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    eq = same_bits(gpu[..., :3], cpu[..., :3])
+    assert eq.all(), "%d samples differ" % (~eq.all(axis=-1)).sum()
