@@ -87,7 +87,7 @@ struct rmr_ctx {
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
     int shade_threshold = 16;
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
-    int full_threshold = 48;    // nearest-primitive cache: lanes per full map() batch (BVH scenes; tuned on csg256)
+    int full_threshold = 40;    // nearest-primitive cache: lanes per full map() batch (BVH scenes; tuned on csg256)
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of

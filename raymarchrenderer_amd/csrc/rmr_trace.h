@@ -77,7 +77,7 @@ struct Lane {
     // nearest-primitive cache (MAP::kCache, see npc_* below): leaf-order index of the last exact
     // minimiser, lower bound of every other primitive's distance minus the error terms (relative to
     // the anchor point), and the anchor's ray parameter t
-    int cw;
+    int cw, cw2;   // (cw2: the second cached primitive when RMR_NPC_K == 2, else == cw)
     float cs, cta;
     float texit;   // escape bound of the current ray (ray_exit)
 };
@@ -478,21 +478,33 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
     const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
     return (k0 + length(vmax0(qq))) - rad;
 }
-// map_bvh plus the minimiser's leaf index kw (-1: none at or below maxDist, or a NaN) and s2.
-// Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id
-// ms; ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
+// Primitives per lane in the nearest-primitive cache (1 or 2): with 2 the cache holds the two
+// nearest primitives and bounds every other one (a ray passing between two neighbours keeps them).
+#ifndef RMR_NPC_K
+#define RMR_NPC_K 2
+#endif
+// map_bvh plus the cache's primitives kw, kw2 (leaf indices; kw -1: none at or below maxDist, or a
+// NaN) and sb, a lower bound of every other primitive's distance: the smallest exact distance among
+// the evaluated non-cached primitives, or a skipped node's box distance minus the culling margin.
+// Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id ms;
+// ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
 // distance tightens the culling bound from the first node on.
-RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2, int ks, int js, float ds, float ms) {
+RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
     CDPrim* pr = (CDPrim*)P.dprims;
     float dbest = P.max_dist, mbest = -1.0f, mnan = -1.0f;
     int jbest = -1, jnan = -1, kbest = -1;
-    float sec = __builtin_inff();
+    // the three smallest evaluated distances (u1 <= u2 <= u3), the leaf indices of the first two,
+    // and the smallest skipped-node bound
+    float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff(), lbs = __builtin_inff();
+    int k1 = -1, k2 = -1;
     if (ks >= 0) {   // (a NaN ds is never seeded: the caller passes ks = -1)
-        sec = __builtin_amdgcn_fmed3f(dbest, ds, sec);
+        u1 = ds;
+        k1 = ks;
         if (ds <= dbest) { dbest = ds; mbest = ms; jbest = js; kbest = ks; }
     }
+    (void)kbest;
     int i = 0;
     while (i < P.n_nodes) {
         const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
@@ -504,7 +516,7 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2, int ks, int js,
         const bool need = !(lb2 > t * t);   // NaN p: lb2 NaN -> needed
         if (!__ballot(need)) {
             // every primitive below is >= the node box distance - bvh_margin (map_bvh's culling rule)
-            sec = fminf(sec, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+            lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
             i = skip;
             continue;
         }
@@ -518,14 +530,28 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, float& s2, int ks, int js,
             const float mid = pr[k].mat_id;
             if (k == ks) continue;   // the seed, already folded in
             const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
-            sec = __builtin_amdgcn_fmed3f(dbest, dj, sec);   // second smallest (maxDist included: safe)
+            // insert dj into (u1, u2, u3): u3' = med3(u2, dj, u3), u2' = med3(u1, dj, u2), u1' = min
+            const bool lt1 = dj < u1, lt2 = dj < u2;
+            u3 = __builtin_amdgcn_fmed3f(u2, dj, u3);
+            u2 = __builtin_amdgcn_fmed3f(u1, dj, u2);
+            k2 = lt1 ? k1 : (lt2 ? k : k2);
+            k1 = lt1 ? k : k1;
+            u1 = fminf(u1, dj);
             if (dj < dbest || (dj == dbest && j > jbest)) { dbest = dj; mbest = mid; jbest = j; kbest = k; }
             if (dj != dj && j > jnan) { jnan = j; mnan = mid; }
         }
         i = skip;
     }
-    kw = (jnan >= 0 || jbest < 0) ? -1 : kbest;
-    s2 = sec;
+    // the cache is the set {k1, k2} (the fold's own minimiser is one of them when the bound holds)
+    // and the bound covers exactly the primitives outside it
+    kw = (jnan >= 0 || jbest < 0 || k1 < 0) ? -1 : k1;
+    if (RMR_NPC_K >= 2 && k2 >= 0) {
+        kw2 = k2;
+        sb = fminf(u3, lbs);
+    } else {
+        kw2 = k1;
+        sb = fminf(u2, lbs);
+    }
     return v2(dbest, jnan > jbest ? mnan : mbest);
 }
 
@@ -539,8 +565,8 @@ struct TableMap {
         else if constexpr (NP == -2 || NP == -3) return map_bvh(P, p);
         else return map_general(P, p);
     }
-    static RMR_D V2 full(const KParams& P, V3 p, int& kw, float& s2, int ks, int js, float ds, float ms) {
-        return map_bvh_npc(P, p, kw, s2, ks, js, ds, ms);
+    static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+        return map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
 };
 
@@ -760,6 +786,7 @@ RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
     }
     const V3 dir = primary_dir(P, px, py, time, rc);
     L.cw = 0;
+    L.cw2 = 0;
     L.cs = -__builtin_inff();
     if (fresh) {
         L.unit = u;
@@ -807,6 +834,7 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
         return;
     }
     L.cw = 0;
+    L.cw2 = 0;
     L.cs = -__builtin_inff();
     L.unit = u;
     L.time = b.z;
@@ -1361,10 +1389,27 @@ RMR_D void trace_main(const KParams& P) {
                 if (act) {
                     p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
                     F = prim_dist(P, L.cw, p, mid, jw);
+                    float Fm = F;
+                    if (RMR_NPC_K >= 2) {
+                        // both cached primitives, folded in scene order: opU's closed form over the
+                        // pair (every other primitive is strictly farther when the bound holds)
+                        float mid2;
+                        int jw2;
+                        const float F2 = prim_dist(P, L.cw2, p, mid2, jw2);
+                        if (jw2 < jw) {
+                            opu(m, F2, mid2);
+                            opu(m, F, mid);
+                        } else {
+                            opu(m, F, mid);
+                            opu(m, F2, mid2);
+                        }
+                        Fm = fminf(F, F2);
+                    } else {
+                        opu(m, F, mid);
+                    }
                     const float delta = (L.phase == PH_NORMAL) ? NPC_PROBE_DELTA : (L.t - L.cta) * (1.0f + 0x1p-21f);
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
-                    ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > F);
-                    opu(m, F, mid);
+                    ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > Fm);
                 }
                 const uint64_t okm = __ballot(act && ok);
                 const uint64_t fm = __ballot(act && !ok);
@@ -1373,10 +1418,11 @@ RMR_D void trace_main(const KParams& P) {
                 const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
                     if (act && !ok) {
-                        int kw;
+                        int kw, kw2;
                         float s2;
-                        m = MAP::full(P, p, kw, s2, F == F ? L.cw : -1, jw, F, mid);
+                        m = MAP::full(P, p, kw, kw2, s2, F == F ? L.cw : -1, jw, F, mid);
                         L.cw = kw >= 0 ? kw : 0;
+                        L.cw2 = kw >= 0 ? kw2 : 0;
                         // |s2| 2^-20: the rounding of the check's own subtractions
                         L.cs = kw >= 0 ? s2 - fmaf(fabsf(s2), 0x1p-20f, npc_eps(P, p)) -
                                              (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
