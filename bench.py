@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-psnr", action="store_true", help="skip the converged PSNR check vs the reference render")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel", type=int, default=0, help="0 persistent, 1 per-path")
     ap.add_argument("--shade-threshold", type=int, default=0)
@@ -98,6 +99,40 @@ def cpu_baseline(cfg, spp, seconds, threads):
     return {"value": done / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": "%d samples: rows y%%%d==0 of the %dx%d frame, 1 spp per row pass, %d-thread OpenMP C "
                       "restatement (oracle/rmr_oracle.c)" % (done, stride, W, H, threads)}
+
+
+GOLDEN_OF = {"c1": "img_rm1_sphere1_b1.npz", "c2": "img_rm1_cornell5_b4.npz"}
+
+
+def psnr_vs_reference(cfg_name, cfg, device):
+    """PSNR of a converged GPU render against the reference GLSL's own converged render of the same
+    scene (Mesa llvmpipe, tests/golden/, generated by oracle/glsl_ref/make_goldens.py) on the shared
+    small-seed schedule. Outside the timed region; None for configs without one."""
+    import numpy as np
+    from raymarchrenderer_amd import Renderer, abi, parity_schedule
+    name = GOLDEN_OF.get(cfg_name)
+    if not name:
+        return None
+    g = np.load(os.path.join(ROOT, "tests", "golden", name))
+    ref = g["conv"]
+    H, W = ref.shape[:2]
+    n = int(g["spp_conv"])
+    r = Renderer(device, W, H)
+    try:
+        r.load_scene(os.path.join(ROOT, "scenes", cfg["scene"]), "rm1")
+        r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
+        r.set_view(g["view"])
+        r.render_spp(parity_schedule(n))
+        img = r.read_accum()
+    finally:
+        r.close()
+    a = np.clip(img[..., :3].astype(np.float64), 0, 1)
+    b = np.clip(ref[..., :3].astype(np.float64), 0, 1)
+    psnr = 10 * np.log10(1.0 / max(np.mean((a - b) ** 2), 1e-30))
+    rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(float(ref[..., :3].mean()), 1e-12)
+    return {"psnr_db": round(float(psnr), 2), "mean_rel_diff": round(float(rel), 5),
+            "reference": "RayMarch.glsl on Mesa llvmpipe, %dx%d, %d spp (tests/golden/%s)" % (W, H, n, name),
+            "gpu_spp": n}
 
 
 def main():
@@ -196,6 +231,10 @@ def main():
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(cfg, spp, args.cpu_seconds, threads)
 
+    parity = None
+    if rank == 0 and not args.no_psnr:
+        parity = psnr_vs_reference(args.config, cfg, local_rank)
+
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
@@ -205,7 +244,7 @@ def main():
                                       % (cfg["name"], W, H, spp, BOUNCES),
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
                           "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world},
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity}
         print(json.dumps(out), flush=True)
     r.close()
     if dist_on:
