@@ -11,7 +11,7 @@ import numpy as np
 from raymarchrenderer_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("RMR_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")   # (sanitizer test)
 _lib = None
 
 
