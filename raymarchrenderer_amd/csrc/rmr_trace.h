@@ -1297,6 +1297,9 @@ constexpr int trace_waves() {
     return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
 }
 
+#ifndef RMR_INNER_MARCH
+#define RMR_INNER_MARCH 1
+#endif
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
@@ -1441,14 +1444,23 @@ RMR_D void trace_main(const KParams& P) {
                 iters += dm ? 1 : 0;
             }
         } else if (amask) {
-            if (act) {
-                const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
-                const V2 m = MAP::eval(P, p);
-                if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                else march_update<HO>(P, L, m);
+            // map() steps back to back until a shading batch is due or no lane is active: idle lanes
+            // only appear in shading and refill, so the refill / restart checks can wait until then
+            uint64_t am = amask;
+            for (;;) {
+                if (is_active(L.phase)) {
+                    const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
+                    const V2 m = MAP::eval(P, p);
+                    if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                    else march_update<HO>(P, L, m);
+                }
+                maps += (uint64_t)__popcll(am);
+                iters++;
+                if (!RMR_INNER_MARCH) break;
+                const uint64_t sm = __ballot(is_shade(L.phase));
+                am = __ballot(is_active(L.phase));
+                if (!am || __popcll(sm) >= T) break;
             }
-            maps += (uint64_t)__popcll(amask);
-            iters++;
         }
         RMR_STAMP(c2);
         const uint64_t smask = __ballot(is_shade(L.phase));
