@@ -1381,7 +1381,8 @@ RMR_D void trace_main(const KParams& P) {
         const bool act = is_active(L.phase);
         const uint64_t amask = __ballot(act);
         if constexpr (MAP::kCache && HO) {   // HO kernels only: normalized directions, fixed bounce offsets
-            if (amask) {
+            for (bool go = amask != 0; go;) {   // inner march loop (see the non-cache path)
+                const bool act1 = is_active(L.phase);
                 // nearest-primitive cache: one primitive where the bound holds; lanes where it does not
                 // wait for a full map() batch (>= full_threshold lanes, or no lane could use the cache)
                 V3 p = v3s(0.0f);
@@ -1389,7 +1390,7 @@ RMR_D void trace_main(const KParams& P) {
                 bool ok = false;
                 float F = 0.0f, mid = -1.0f;
                 int jw = 0;
-                if (act) {
+                if (act1) {
                     p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
                     F = prim_dist(P, L.cw, p, mid, jw);
                     float Fm = F;
@@ -1414,13 +1415,13 @@ RMR_D void trace_main(const KParams& P) {
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
                     ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > Fm);
                 }
-                const uint64_t okm = __ballot(act && ok);
-                const uint64_t fm = __ballot(act && !ok);
+                const uint64_t okm = __ballot(act1 && ok);
+                const uint64_t fm = __ballot(act1 && !ok);
                 bool done = ok;
                 const int nf = __popcll(fm), nok = __popcll(okm);
                 const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
-                    if (act && !ok) {
+                    if (act1 && !ok) {
                         int kw, kw2;
                         float s2;
                         m = MAP::full(P, p, kw, kw2, s2, F == F ? L.cw : -1, jw, F, mid);
@@ -1442,6 +1443,8 @@ RMR_D void trace_main(const KParams& P) {
                 const uint64_t dm = __ballot(done);
                 maps += (uint64_t)__popcll(dm);
                 iters += dm ? 1 : 0;
+                const uint64_t sm = __ballot(is_shade(L.phase));
+                go = RMR_INNER_MARCH && __ballot(is_active(L.phase)) && __popcll(sm) < T;
             }
         } else if (amask) {
             // map() steps back to back until a shading batch is due or no lane is active: idle lanes
