@@ -317,6 +317,39 @@ RMR_D void am_sphere(AMin& m, V3 p, V3 c, float r, float id) {
     const float l2 = dot(v, v);
     am_take(m, __builtin_amdgcn_sqrtf(l2) - r, l2, -r, id);
 }
+// Boxes fold without a sqrt each: sd_box = k + length(max(q, 0)) has k = 0 when the point is outside
+// (len2 > 0) and len2 = 0 inside, so the key (len2 outside, k <= 0 inside, NaN for a NaN point)
+// orders boxes as their distances do (sqrt_cr is monotonic). The two smallest keys become the
+// approximate minimum and runner-up (one bare v_sqrt_f32 each), which the spheres then fold into:
+// every other box's exact distance is >= the runner-up key's, so am_unique's bound is unchanged.
+struct BMin {
+    float k1, k2, id;
+};
+RMR_D float bm_key(V3 p, V3 c, V3 r) {
+    const V3 q = vabs(p - c) - r;
+    const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
+    const V3 o = vmax0(q);
+    const float l2 = dot(o, o);
+    return (l2 > 0.0f || l2 != l2) ? l2 : k;
+}
+RMR_D void bm_box0(BMin& b, V3 p, V3 c, V3 r, float id) {
+    b.k1 = bm_key(p, c, r);
+    b.k2 = __builtin_inff();
+    b.id = id;
+}
+RMR_D void bm_box(BMin& b, V3 p, V3 c, V3 r, float id) {
+    const float key = bm_key(p, c, r);
+    b.k2 = __builtin_amdgcn_fmed3f(b.k1, key, b.k2);
+    const bool t = key < b.k1;
+    b.k1 = t ? key : b.k1;
+    b.id = t ? id : b.id;
+}
+RMR_D float bm_dist(float key) { return key > 0.0f ? __builtin_amdgcn_sqrtf(key) : key; }
+RMR_D void am_boxes(AMin& m, const BMin& b) {
+    const bool out = b.k1 > 0.0f;
+    am_first(m, bm_dist(b.k1), out ? b.k1 : 0.0f, out ? 0.0f : b.k1, b.id);
+    m.s2 = bm_dist(b.k2);
+}
 // true when the minimiser is certain (see above); false for near ties, NaN and infinite values, and
 // for a minimiser whose len2 is in sqrt_cr's tiny range (0 < len2 < 2^-96: the exact fold handles it)
 RMR_D bool am_unique(const AMin& m, float R2) {   // R2 = 2 R
@@ -1305,7 +1338,7 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
-    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0;
+    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
     constexpr uint32_t CHUNK = 128;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
@@ -1470,6 +1503,7 @@ RMR_D void trace_main(const KParams& P) {
         const uint64_t amask2 = __ballot(is_active(L.phase));
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
+            shaded += (uint64_t)__popcll(smask);
             if (is_shade(L.phase)) shade<VAR, PROG, MATS>(P, L);
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
@@ -1488,6 +1522,7 @@ RMR_D void trace_main(const KParams& P) {
         atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
         atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
         if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
+        atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);

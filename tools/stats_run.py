@@ -2,6 +2,7 @@
 (map evals, map iterations, shading batches, trace ms). Run under rocprofv3 --pmc for per-launch
 instruction counts (tools/pmc_sweep.sh)."""
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -9,6 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
+from raymarchrenderer_amd._lib import lib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=16)
@@ -24,6 +26,10 @@ r.render_spp(time_schedule(a.spp))   # warm-up (JIT compile)
 r.reset_stats()
 r.render_spp(time_schedule(a.spp))
 st = r.stats()
+raw = (C.c_uint64 * 16)()
+lib().rmr_get_counters(r._ctx, raw)
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("RMR_")}, "trace_ms": round(st.trace_ms, 3),
-                  "map_evals": st.map_evals, "map_iters": st.map_iters, "shade_batches": st.shade_batches}))
+                  "map_evals": st.map_evals, "map_iters": st.map_iters, "shade_batches": st.shade_batches,
+                  "lanes_shaded": raw[8], "lanes_per_batch": round(raw[8] / max(1, st.shade_batches), 2),
+                  "evals_per_iter": round(st.map_evals / max(1, st.map_iters), 2)}))
 r.close()
