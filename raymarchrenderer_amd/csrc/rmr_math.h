@@ -154,6 +154,9 @@ RMR_D float acos_R(float z) {
     float q = 1.0f + z * -7.0662963390e-01f;
     return p / q;
 }
+// The three argument ranges share one acos_R and one sqrt_cr on the range's own z (the same
+// operations per lane as the branchy form, so the same bits; a wave with lanes in all three ranges
+// runs the rational once instead of three times).
 RMR_D float det_acos(float x) {
     const float pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
     uint32_t hx = __float_as_uint(x), ix = hx & 0x7fffffffu;
@@ -161,21 +164,19 @@ RMR_D float det_acos(float x) {
         if (ix == 0x3f800000u) return (hx >> 31) ? 3.14159274101257324219f : 0.0f;
         return __uint_as_float(0x7fc00000u);
     }
-    if (ix < 0x3f000000u) {
-        if (ix <= 0x32800000u) return 1.57079637050628662109375f;
-        return pio2_hi - (x - (pio2_lo - x * acos_R(x * x)));
-    }
-    if (hx >> 31) {
-        float z = (1.0f + x) * 0.5f;
-        float s = sqrt_cr(z);
-        float w = acos_R(z) * s - pio2_lo;
+    const bool small = ix < 0x3f000000u, neg = (hx >> 31) != 0;
+    if (small && ix <= 0x32800000u) return 1.57079637050628662109375f;
+    const float z = small ? x * x : (neg ? (1.0f + x) * 0.5f : (1.0f - x) * 0.5f);
+    const float R = acos_R(z);
+    if (small) return pio2_hi - (x - (pio2_lo - x * R));
+    const float s = sqrt_cr(z);
+    if (neg) {
+        float w = R * s - pio2_lo;
         return 2.0f * (pio2_hi - (s + w));
     }
-    float z = (1.0f - x) * 0.5f;
-    float s = sqrt_cr(z);
     float df = __uint_as_float(__float_as_uint(s) & 0xfffff000u);
     float c = (z - df * df) / (s + df);
-    float w = acos_R(z) * s + c;
+    float w = R * s + c;
     return 2.0f * (df + w);
 }
 
@@ -237,14 +238,15 @@ RMR_D float det_atan(float x) {
     if (inv) r = 1.57079637050628662109375f - r;
     return (x < 0.0f) ? -r : r;
 }
+// (one division and one det_atan for both octant cases: the same operations per lane as
+// r = |x| >= |y| ? atan(y / x) (+-pi) : +-pi/2 - atan(x / y))
 RMR_D float det_atan2(float y, float x) {
     if (x == 0.0f && y == 0.0f) return 0.0f;
-    float r;
-    if (fabsf(x) >= fabsf(y)) {
-        r = det_atan(y / x);
+    const bool xa = fabsf(x) >= fabsf(y);
+    float r = det_atan((xa ? y : x) / (xa ? x : y));
+    if (xa) {
         if (x < 0.0f) r = (y < 0.0f) ? r - 3.14159274101257324219f : r + 3.14159274101257324219f;
     } else {
-        r = det_atan(x / y);
         r = ((y < 0.0f) ? -1.57079637050628662109375f : 1.57079637050628662109375f) - r;
     }
     return r;

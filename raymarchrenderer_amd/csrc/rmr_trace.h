@@ -114,8 +114,9 @@ RMR_D V3 hemisphere(Lane& L, V2 s1, V2 s2, V3 n) {
     V3 b = normalize(v3(sp * ct, cp, sp * st));
     if (!is_zero(n)) {
         if (b.z < 0.0f) b = -b;
-        V3 lx = veq(n, v3(0.0f, 1.0f, 0.0f)) ? normalize(cross(n, v3(0.0f, 0.0f, 1.0f)))
-                                              : normalize(cross(n, v3(0.0f, 1.0f, 0.0f)));
+        // one cross + normalize with the axis selected per lane (same operations as the two-sided form)
+        const bool up = veq(n, v3(0.0f, 1.0f, 0.0f));
+        V3 lx = normalize(cross(n, v3(0.0f, up ? 0.0f : 1.0f, up ? 1.0f : 0.0f)));
         V3 ly = normalize(cross(n, lx));
         b = mat_mul(lx, ly, n, b);
     }
