@@ -935,6 +935,18 @@ RMR_D V3 probe_point(const Lane& L) {
     const V3 hp = hitref<HO>(L);
     return v3(hp.x + (ax == 0 ? hs : z0), hp.y + (ax == 1 ? hs : z0), hp.z + (ax == 2 ? hs : z0));
 }
+// The map() point of an active lane without a divergent branch: march points are fma(d, t, o); a
+// probe is hit + e as fma(e, 1, hit), which is the same rounded add bit for bit (e * 1 is exact).
+template <bool HO>
+RMR_D V3 march_point(const Lane& L) {
+    const bool nrm = (L.phase == PH_NORMAL);
+    const int ax = L.ctr >> 1;
+    const bool neg = (L.ctr & 1) != 0;
+    const float h = 0.001f, hs = neg ? -h : h, z0 = neg ? -0.0f : 0.0f;
+    const V3 D = nrm ? v3(ax == 0 ? hs : z0, ax == 1 ? hs : z0, ax == 2 ? hs : z0) : L.d;
+    const float T = nrm ? 1.0f : L.t;
+    return vfma(D, T, HO ? L.o : (nrm ? L.hit : L.o));
+}
 // nrm.c holds map(p + h e_c) after the + probe and map(p + h e_c) - map(p - h e_c) after the - probe
 RMR_D void normal_update(Lane& L, float m) {
     const int ax = L.ctr >> 1;
@@ -1331,6 +1343,14 @@ constexpr int trace_waves() {
     return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
 }
 
+#ifndef RMR_UNIFIED_POINT
+#define RMR_UNIFIED_POINT 1
+#endif
+#if RMR_UNIFIED_POINT   // HO kernels (A/B: C2 +1%; the RM2 kernel was slower with it)
+#define RMR_MARCH_POINT(L) (HO ? march_point<HO>(L) : ((L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o)))
+#else
+#define RMR_MARCH_POINT(L) ((L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o))
+#endif
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
 #endif
@@ -1425,7 +1445,7 @@ RMR_D void trace_main(const KParams& P) {
                 float F = 0.0f, mid = -1.0f;
                 int jw = 0;
                 if (act1) {
-                    p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
+                    p = RMR_MARCH_POINT(L);
                     F = prim_dist(P, L.cw, p, mid, jw);
                     float Fm = F;
                     if (RMR_NPC_K >= 2) {
@@ -1486,7 +1506,7 @@ RMR_D void trace_main(const KParams& P) {
             uint64_t am = amask;
             for (;;) {
                 if (is_active(L.phase)) {
-                    const V3 p = (L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o);
+                    const V3 p = RMR_MARCH_POINT(L);
                     const V2 m = MAP::eval(P, p);
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO>(P, L, m);
