@@ -888,8 +888,29 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
 // distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
+#ifndef RMR_BRANCHLESS_UPDATE
+#define RMR_BRANCHLESS_UPDATE 1
+#endif
 template <bool HO, bool CACHE = false>
 RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
+    if constexpr (HO && !CACHE && RMR_BRANCHLESS_UPDATE) {   // (cache kernels: A/B neutral-negative)
+        // HO kernels (no shadow rays): the same state transitions as below as per-lane selects
+        const float dist = L.inside ? -m.x : m.x;
+        const bool hit = dist < 0.001f;
+        const bool past = L.t >= P.max_dist;
+        const float tn = fmaf(dist, P.step_mult, L.t);
+        const int cn = L.ctr + 1;
+        const bool miss = !hit && (past || cn >= P.max_steps || tn > L.texit);
+        const float tf = hit ? L.t : (miss ? P.max_dist : tn);
+        const bool fin = hit || miss;
+        const V3 hp = vfma(L.d, tf, L.o);
+        L.o = v3(fin ? hp.x : L.o.x, fin ? hp.y : L.o.y, fin ? hp.z : L.o.z);
+        L.t = tf;
+        L.mid = hit ? m.y : (miss ? -1.0f : L.mid);
+        L.ctr = hit ? 0 : cn;
+        L.phase = hit ? PH_NORMAL : (miss ? PH_MISS : L.phase);
+        return;
+    }
     const bool shadow = (L.phase == PH_SHADOW);
     const float dist = (L.inside && !shadow) ? -m.x : m.x;
     if (dist < 0.001f) {
