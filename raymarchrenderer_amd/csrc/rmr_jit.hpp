@@ -22,6 +22,7 @@ struct JitKernel {
     hipModule_t module = nullptr;
     hipFunction_t fn = nullptr;
     int blocks_per_cu = 0;
+    int shade_t = 16;           // default shading batch size for this kernel (rmr_api.cpp)
 };
 
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the
