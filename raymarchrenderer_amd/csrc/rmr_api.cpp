@@ -88,7 +88,7 @@ struct rmr_ctx {
     int shade_threshold = 16;   // explicit (env RMR_SHADE_T / rmr_set_tuning) or, with shade_auto, per kernel:
     bool shade_auto = true;     // 20 for RM1 inline sphere/box specialisations (C2), 16 otherwise
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
-    int full_threshold = 40;    // nearest-primitive cache: lanes per full map() batch (BVH scenes; tuned on csg256)
+    int full_threshold = 40 | (2 << 8);   // nearest-primitive cache: 40 lanes per full map() batch, R = 2 (csg256)
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
@@ -721,8 +721,10 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
     if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
     if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
-    if (const char* e = std::getenv("RMR_FULL_T")) c->full_threshold = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RMR_FULL_R")) c->full_threshold |= std::max(0, std::min(255, std::atoi(e))) << 8;
+    if (const char* e = std::getenv("RMR_FULL_T"))
+        c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RMR_FULL_R"))
+        c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
