@@ -242,3 +242,29 @@ def test_culling_switches_bitexact(renderer, scene, bounces, spp):
     for k, img in out.items():
         assert np.array_equal(ref, img.view(np.uint32)), k
     assert evals[(1, abi.CULL_ALL)] < evals[(1, 0)] == evals[(0, 0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["cornell5.scene", "csg256.scene"])
+def test_scheduling_knobs_bitexact(scene):
+    """Shading-batch size, refill threshold and persistent grid size (rmr_set_tuning) decide only
+    which lanes run which path when: the image is bitwise the same for every setting, including the
+    per-kernel default (20-lane batches on Cornell-5, 16 on the cached BVH kernel)."""
+    from raymarchrenderer_amd import Renderer
+    W, H = 160, 96
+    r = Renderer(0, 64, 64)   # own context: the settings below would outlive the test
+    try:
+        r.set_jit(1)
+        _setup(r, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
+        times = time_schedule(6, frame=3)
+        imgs = []
+        for shade, grid in ((0, -1), (1, -1), (7 | (3 << 8), 2), (20, -1), (64 | (64 << 8), 1), (33, 5)):
+            if shade:
+                r.set_tuning(shade, grid)
+            r.reload()
+            r.render_spp(times)
+            imgs.append(r.read_accum().view(np.uint32).copy())
+    finally:
+        r.close()
+    for k, img in enumerate(imgs[1:], 1):
+        assert np.array_equal(imgs[0], img), k
