@@ -523,7 +523,7 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
 // Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id ms;
 // ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
 // distance tightens the culling bound from the first node on.
-RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
     CDPrim* pr = (CDPrim*)P.dprims;
@@ -587,6 +587,98 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         sb = fminf(u2, lbs);
     }
     return v2(dbest, jnan > jbest ? mnan : mbest);
+}
+
+// The same traversal on approximate distances (am_* above: bare v_sqrt_f32, |a - d| <= 2^-21 (|a| +
+// R) + 2^-40), without the exact fold's minimum / tie / NaN bookkeeping, then the minimiser's exact
+// distance once. Where the two smallest approximate values are separated by am_unique's margin the
+// approximate minimiser is the exact fold's unique minimiser, so the result is opU((maxDist, -1),
+// d_w, id_w) (closed form, as am_result) and the cache is {k1, k2} as in map_bvh_npc_exact; the
+// bound sb takes the third-smallest approximate value minus twice its error bound (or a skipped
+// node's bound). The culling radius is an upper bound of the exact running minimum (the approximate
+// one plus twice its error bound), so no node the exact traversal needs is skipped, and a skipped
+// node's primitives stay strictly above the exact minimum. Lanes without that separation (near
+// ties, NaN or infinite points) run map_bvh_npc_exact: the results are the exact traversal's.
+RMR_D float am_prim(int type, V3 p, V3 c, V3 r) {
+    if (type == RMR_PRIM_BOX) {
+        const V3 q = vabs(p - c) - r;
+        const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
+        const V3 o = vmax0(q);
+        return k + __builtin_amdgcn_sqrtf(dot(o, o));
+    }
+    const V3 v = p - c;
+    return __builtin_amdgcn_sqrtf(dot(v, v)) - r.x;
+}
+#ifndef RMR_NPC_APPROX
+#define RMR_NPC_APPROX 1
+#endif
+RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+    if (!RMR_NPC_APPROX) return map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
+    typedef const __attribute__((address_space(4))) BvhNode CNode;
+    CNode* nodes = (CNode*)P.bvh;
+    CDPrim* pr = (CDPrim*)P.dprims;
+    const float R2 = P.am_r2;
+    // the three smallest approximate distances (u1 <= u2 <= u3), the leaf indices of the first two,
+    // and the smallest skipped-node bound; the seed's distance is exact
+    float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff(), lbs = __builtin_inff();
+    int k1 = -1, k2 = -1;
+    if (ks >= 0) {
+        u1 = ds;
+        k1 = ks;
+    }
+    int i = 0;
+    while (i < P.n_nodes) {
+        const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
+        const V3 hi = v3(nodes[i].hi[0], nodes[i].hi[1], nodes[i].hi[2]);
+        const int count = nodes[i].count, skip = nodes[i].skip;
+        const V3 q = vmax0(vmax(lo - p, p - hi));
+        const float lb2 = dot(q, q);
+        // >= the exact running minimum (capped at maxDist as the exact fold's dbest)
+        const float ub = fminf(P.max_dist, u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f));
+        const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
+        const bool need = !(lb2 > t * t);
+        if (!__ballot(need)) {
+            lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+            i = skip;
+            continue;
+        }
+        if (count == 0) { i++; continue; }
+        const int first = nodes[i].first;
+        for (int k = first; k < first + count; k++) {
+            const int type = pr[k].type & 0xff;
+            const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
+            const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
+            if (k == ks) continue;
+            const float a = am_prim(type, p, c, r);
+            const bool lt1 = a < u1, lt2 = a < u2;
+            u3 = __builtin_amdgcn_fmed3f(u2, a, u3);
+            u2 = __builtin_amdgcn_fmed3f(u1, a, u2);
+            k2 = lt1 ? k1 : (lt2 ? k : k2);
+            k1 = lt1 ? k : k1;
+            u1 = fminf(u1, a);
+        }
+        i = skip;
+    }
+    const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
+    const bool uniq = (u2 - u1 > margin) && k1 >= 0;
+    V2 d = v2(P.max_dist, -1.0f);
+    if (uniq) {
+        float mid;
+        int j;
+        const float dw = (k1 == ks) ? ds : prim_dist(P, k1, p, mid, j);
+        if (k1 == ks) mid = ms;
+        opu(d, dw, mid);
+        kw = (dw > P.max_dist) ? -1 : k1;   // (the exact fold: no primitive at or below maxDist)
+        // lower bound of an approximate value's exact distance (twice the error bound)
+        const float v = (RMR_NPC_K >= 2 && k2 >= 0) ? u3 : u2;
+        const float vlb = v - fmaf(fabsf(v) + R2, 0x1p-20f, 0x1p-39f);
+        kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
+        sb = fminf(vlb, lbs);
+    }
+    if (__ballot(!uniq)) {
+        if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
+    }
+    return d;
 }
 
 template <int NP>
