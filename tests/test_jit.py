@@ -165,6 +165,42 @@ def test_jit_approx_map_ties_bitexact(renderer):
     assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
 
 
+def _bvh_ties_scene():
+    """_ties_scene padded past the inline-map limit (32 primitives) with small spheres above the
+    box, so the BVH map with the nearest-primitive cache runs: its approximate traversal
+    (rmr_trace.h map_bvh_npc) meets exact ties everywhere on the duplicated sphere and floor and has
+    to take its exact fallback there."""
+    import json
+    sc = _ties_scene()
+    ball = sc["objects"][3]
+    for n in range(30):
+        pad = json.loads(json.dumps(ball))
+        pad["nodes"][0]["inputs"][1] = [-3.0 + 0.2 * n, 9.0 + 0.1 * (n % 3), -2.0 + 0.13 * n]
+        pad["nodes"][0]["inputs"][2] = [0.05, 0.05, 0.05]
+        sc["objects"].append(pad)
+    assert len(sc["objects"]) > 32
+    return sc
+
+
+@pytest.mark.gpu
+def test_jit_bvh_cache_ties_bitexact_vs_oracle(renderer):
+    sc = _bvh_ties_scene()
+    W, H = 48, 40
+    rect = (0, 0, W, H)
+    prm, view = _setup(renderer, sc, "rm1", W, H, {"max_bounces": 4})
+    renderer.set_jit(1)
+    try:
+        times = time_schedule(3, frame=4)
+        gpu = renderer.trace_samples(times, rect)
+        assert renderer.stats().jit_launches > 0
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(scene_compile.compile_scene(sc, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
 @pytest.mark.gpu
 def test_jit_bvh_nearest_primitive_cache_matches_table_kernel(renderer):
     """csg256 (256 primitives, BVH map): the JIT kernel with the nearest-primitive cache (one
