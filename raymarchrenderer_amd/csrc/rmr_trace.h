@@ -1447,9 +1447,10 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 #ifndef RMR_FAST_WAVES
 #define RMR_FAST_WAVES 8
 #endif
-// waves/SIMD the register allocator targets (launch bounds of the kernels that call trace_main)
+// waves/SIMD the register allocator targets for the general-map (node program, Mandelbulb) kernels
+// without material programs (A/B on C3: 8 waves +8% over the allocator's free choice)
 #ifndef RMR_GENERAL_WAVES
-#define RMR_GENERAL_WAVES 1
+#define RMR_GENERAL_WAVES 8
 #endif
 template <int VAR, bool GENERAL, bool PROG>
 constexpr int trace_waves() {
