@@ -86,7 +86,7 @@ struct rmr_ctx {
     rmr_stats stats{};
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
     int shade_threshold = 16;   // explicit (env RMR_SHADE_T / rmr_set_tuning) or, with shade_auto, per kernel:
-    bool shade_auto = true;     // 20 for RM1 inline sphere/box specialisations (C2), 16 otherwise
+    bool shade_auto = true;     // per specialised kernel (ensure_jit: 20 / 8 / 16), 16 for the table kernels
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
     int full_threshold = 40 | (2 << 8);   // nearest-primitive cache: 40 lanes per full map() batch, R = 2 (csg256)
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
@@ -332,8 +332,14 @@ int ensure_jit(rmr_ctx* c) {
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, 256, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
-    k.shade_t = (src.find("rmr::trace_waves<1, false, false>") != std::string::npos &&
-                 src.find("TableMap<") == std::string::npos) ? 20 : 16;
+    // RM1 inline sphere/box maps: 20 (C2 +2%); general maps without material programs, whose
+    // map() dwarfs the shading (the Mandelbulb): 8 (C3 +2-3%); otherwise 16
+    if (src.find("rmr::trace_waves<1, false, false>") != std::string::npos && src.find("TableMap<") == std::string::npos)
+        k.shade_t = 20;
+    else if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
+        k.shade_t = 8;
+    else
+        k.shade_t = 16;
     c->jit_loaded.push_back(k);
     c->jit = k;
     c->jit_ready = true;
