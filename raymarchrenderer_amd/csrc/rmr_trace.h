@@ -131,7 +131,17 @@ RMR_D float sd_box(V3 p, V3 c, V3 r) {                                          
     V3 q = vabs(p - c) - r;
     return fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f) + length(vmax0(q));
 }
-__device__ __noinline__ float sd_mandelbulb(V3 p, V3 c, V3 prm) {
+// inlined into the scene-specialised kernels (hipRTC, rmr_jit.cpp: C3 +4%); a call in the
+// table-driven general kernel (inlining it into the node interpreter measured 4% slower)
+#ifndef RMR_MANDELBULB_INLINE
+#define RMR_MANDELBULB_INLINE 0
+#endif
+#if RMR_MANDELBULB_INLINE
+#define RMR_MB_ATTR __device__ __forceinline__
+#else
+#define RMR_MB_ATTR __device__ __noinline__
+#endif
+RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm) {
     V3 p0 = p - c, z = p0;
     float power = prm.x, bail = prm.z;
     int iters = (int)prm.y;
