@@ -240,10 +240,23 @@ RMR_D float det_atan(float x) {
 }
 // (one division and one det_atan for both octant cases: the same operations per lane as
 // r = |x| >= |y| ? atan(y / x) (+-pi) : +-pi/2 - atan(x / y))
+// det_atan for |x| <= 1 or NaN (its a > 1 branch is never taken there: the same bits, no division)
+RMR_D float det_atan_unit(float x) {
+    float t = fabsf(x);
+    float s = t * t;
+    float p = fmaf(s, -0.0117212f, 0.05265332f);
+    p = fmaf(s, p, -0.11643287f);
+    p = fmaf(s, p, 0.19354346f);
+    p = fmaf(s, p, -0.33262347f);
+    p = fmaf(s, p, 0.99997726f);
+    float r = t * p;
+    return (x < 0.0f) ? -r : r;
+}
 RMR_D float det_atan2(float y, float x) {
     if (x == 0.0f && y == 0.0f) return 0.0f;
     const bool xa = fabsf(x) >= fabsf(y);
-    float r = det_atan((xa ? y : x) / (xa ? x : y));
+    // |num| <= |den|, so the rounded quotient is in [-1, 1] (or NaN for inf / inf)
+    float r = det_atan_unit((xa ? y : x) / (xa ? x : y));
     if (xa) {
         if (x < 0.0f) r = (y < 0.0f) ? r - 3.14159274101257324219f : r + 3.14159274101257324219f;
     } else {
