@@ -1475,6 +1475,9 @@ constexpr int trace_waves() {
 #else
 #define RMR_MARCH_POINT(L) ((L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o))
 #endif
+#ifndef RMR_CHUNK
+#define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
+#endif
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
 #endif
@@ -1484,7 +1487,7 @@ RMR_D void trace_main(const KParams& P) {
     Lane L;
     L.phase = PH_IDLE;
     uint64_t maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
-    constexpr uint32_t CHUNK = 128;
+    constexpr uint32_t CHUNK = RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
     bool exhausted = false;

@@ -9,7 +9,14 @@ expensive (floor, walls) tiles.
 Frames are pipelined over two accumulators: frame f's reduce runs (async, on the collective's own
 stream) while frame f + 1 renders into the other buffer; a buffer is reused only after its reduce
 completed. The reduce of every frame is still one collective over the whole frame.
+
+With two renderer contexts on two HIP streams (`renderer=[r0, r1]`, `streams=[s0, s1]`) consecutive
+frames also overlap on the GPU: the persistent trace kernel of frame f ends with a drain (its last,
+longest paths run on a nearly idle chip, ~1.4 ms on C2), which frame f + 1's kernel, launched on the
+other stream, fills. Each frame's zeroing, render and reduce stay ordered on its own stream.
 """
+import contextlib
+
 import numpy as np
 
 
@@ -43,9 +50,13 @@ class FrameRenderer:
     `renderer`: a raymarchrenderer_amd.Renderer (the accumulator is bound with rmr_bind_accum), or
     None with `render_fn(acc, tiles, times, first_sample)` (tests: the CPU oracle under gloo)."""
 
-    def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None):
-        self.r, self.dist, self.render_fn = renderer, dist, render_fn
+    def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None):
+        self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
+        self.r, self.dist, self.render_fn = self.rs[0], dist, render_fn
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
+        if len(self.accs) % len(self.rs):
+            raise ValueError("accumulators must be a multiple of the renderers")
+        self.streams = list(streams) if streams is not None else None
         self.work = [None] * len(self.accs)
         self.tiles = tile_partition(W, H, tile, rank, world)
         self.tile = tile
@@ -57,25 +68,38 @@ class FrameRenderer:
         accumulator (complete on rank 0 once `finish()` or the next reuse of the buffer waited)."""
         i = self.f % len(self.accs)
         acc = self.accs[i]
-        if self.work[i] is not None:  # the reduce of the frame that last used this buffer
-            self.work[i].wait()
-            self.work[i] = None
-        acc.zero_()
-        if len(self.tiles):
-            if self.render_fn is not None:
-                self.render_fn(acc, self.tiles, times, first_sample)
-            else:
-                self.r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
-                self.r.render_tiles(times, self.tiles, self.tile, first_sample=first_sample)
-        self.work[i] = reduce_frame(acc, self.dist, async_op=True)
+        r = self.next_renderer()
+        with self._on_stream(self.f):
+            if self.work[i] is not None:  # the reduce of the frame that last used this buffer
+                self.work[i].wait()
+                self.work[i] = None
+            acc.zero_()
+            if len(self.tiles):
+                if self.render_fn is not None:
+                    self.render_fn(acc, self.tiles, times, first_sample)
+                else:
+                    r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
+                    r.render_tiles(times, self.tiles, self.tile, first_sample=first_sample)
+            self.work[i] = reduce_frame(acc, self.dist, async_op=True)
         self.f += 1
         self.last = acc
         return acc
+
+    def next_renderer(self):
+        """The renderer context the next frame() uses (e.g. to load that frame's scene)."""
+        return self.rs[self.f % len(self.rs)]
+
+    def _on_stream(self, f):
+        if not self.streams:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(self.streams[f % len(self.streams)])
 
     def finish(self):
         """Wait for every outstanding reduce; returns the last frame's accumulator."""
         for i, w in enumerate(self.work):
             if w is not None:
-                w.wait()
+                with self._on_stream(i):
+                    w.wait()
                 self.work[i] = None
         return self.last
