@@ -110,3 +110,42 @@ def test_gloo_two_ranks_pipelined_frames_exact():
     for got, f in ((f2, 2), (f1, 1)):
         want = _render_tiles(frame_tiles(W, H, TILE), time_schedule(2, frame=f))
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f
+
+
+@pytest.mark.gpu
+def test_overlapped_frames_two_streams_bitexact():
+    """bench.py --overlap: frames alternate between two renderer contexts on two HIP streams
+    (FrameRenderer(renderer=[r0, r1], streams=[s0, s1])), so consecutive frames run concurrently.
+    Every frame's image equals the one-context, one-stream schedule bit for bit."""
+    from raymarchrenderer_amd import Renderer
+    W, H, tile = 96, 64, 32
+    scene = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scenes", "cornell5.scene")
+
+    def run(n_ctx):
+        rs, streams = [], []
+        for _ in range(n_ctx):
+            r = Renderer(0, W, H)
+            r.set_jit(1)
+            r.load_scene(scene, "rm1")
+            r.set_params(abi.default_params(max_bounces=4))
+            s = torch.cuda.Stream() if n_ctx > 1 else torch.cuda.current_stream()
+            r.set_stream(s.cuda_stream)
+            rs.append(r)
+            streams.append(s)
+        accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+        fr = FrameRenderer(rs, accs, W, H, tile, 0, 1, streams=streams if n_ctx > 1 else None)
+        out = []
+        for f in range(4):
+            acc = fr.frame(time_schedule(3, frame=f))
+            if f % 2 == 1:   # both buffers hold finished frames after the odd ones
+                fr.finish()
+                torch.cuda.synchronize()
+                out.append(accs[0].cpu().numpy().view(np.uint32).copy())
+                out.append(acc.cpu().numpy().view(np.uint32).copy())
+        for r in rs:
+            r.close()
+        return out
+
+    one, two = run(1), run(2)
+    for a, b in zip(one, two):
+        assert np.array_equal(a, b)
