@@ -1,5 +1,5 @@
 """Diagnostics: how often the approximate-then-exact map (rmr_trace.h am_*) falls back to the exact
-fold, per scene (RMR_JIT_AMBCOUNT=1 build of the JIT source; counters via rmr_get_section_cycles)."""
+fold, per scene (RMR_JIT_AMBCOUNT=1 build of the JIT source; raw counters [4], [5] via rmr_get_counters)."""
 import ctypes as C
 import json
 import os
@@ -22,8 +22,9 @@ for name, path, b in [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"
     r.reset_stats()
     r.render_spp(time_schedule(4))
     st = r.stats()
-    out = (C.c_uint64 * 4)()
-    lib().rmr_get_section_cycles(r._ctx, out)
+    raw = (C.c_uint64 * 16)()
+    lib().rmr_get_counters(r._ctx, raw)
+    out = [raw[4], raw[5]]
     print(json.dumps({"scene": name, "map_evals": st.map_evals, "map_iters": st.map_iters,
                       "amb_lanes": out[0], "amb_waves": out[1],
                       "amb_lane_frac": out[0] / max(1, st.map_evals), "amb_iter_frac": out[1] / max(1, st.map_iters)}))
