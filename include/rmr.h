@@ -185,7 +185,10 @@ int rmr_set_culling(rmr_ctx* ctx, int flags);
  * scene). On success `log` receives the code-object key, otherwise the compiler log. */
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);
 /* Tuning knobs (<= 0 / < 0 keeps the current value): deferred-shading batch size in lanes (1..64),
- * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. */
+ * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. Until a
+ * batch size is set (here or by env RMR_SHADE_T) it is chosen per kernel: 20 for RM1 sphere/box
+ * specialisations, 8 for general maps without material programs, 16 otherwise. Results do not
+ * depend on any of these (scheduling only). */
 int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long samp_budget_bytes);
 /* (shade_threshold bits 8..15, when non-zero, set the refill threshold separately: idle lanes a
  * wave collects before it fetches new units; default = the shading threshold.) */
