@@ -670,7 +670,10 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         i = skip;
     }
     const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
-    const bool uniq = (u2 - u1 > margin) && k1 >= 0;
+    // no runner-up evaluated (u2 = +inf): every other primitive sits in a skipped node, strictly
+    // above the exact minimum (finite u1: a finite point)
+    const bool alone = (u2 == __builtin_inff()) && (u1 < __builtin_inff());
+    const bool uniq = (alone || u2 - u1 > margin) && k1 >= 0;
     V2 d = v2(P.max_dist, -1.0f);
     if (uniq) {
         float mid;
