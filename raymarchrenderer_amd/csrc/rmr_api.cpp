@@ -280,8 +280,13 @@ int upload_scene(rmr_ctx* c) {
                 op.out[0] != op.out[1] && lit(op.in[0], d.c))
                 d.kind = rmr::MAT_DIFFUSE;
             else if (op.code == RMR_OP_M_EMISSION && m.color_var == op.out[0] && m.dir_var < 0 &&
-                     lit(op.in[0], d.c) && lit(op.in[1], d.p))
+                     lit(op.in[0], d.c) && lit(op.in[1], d.p)) {
                 d.kind = rmr::MAT_EMISSION;
+                // grayscale of p * vec3(1) without separateChannels (rmr_trace.h gray_ch, RM1:306-309):
+                // x * 1 is exact, so this is the kernel's ((p.x + p.y) + p.z) / (1 + 1 + 1)
+                const float sum = (d.p[0] + d.p[1]) + d.p[2];
+                d.gray1 = sum / 3.0f;
+            }
         }
         dm[i] = d;
     }

@@ -30,7 +30,7 @@ struct DMat {
     int32_t kind;
     float c[3];   // diffuse / emission color literal
     float p[3];   // emission power literal
-    int32_t pad;
+    float gray1;  // gray_ch(p, -1) = ((p.x + p.y) + p.z) / 3 (host, same float operations)
 };
 
 // Bounding-volume node of the exact culling map (NP = -2, scenes of more than 32 spheres/boxes).

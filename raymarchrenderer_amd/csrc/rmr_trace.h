@@ -1345,7 +1345,10 @@ RMR_D void shade(const KParams& P, Lane& L) {
             const V3 hp = hitref<HO>(L);
             nd = hemisphere(L, v2(hp.x, hp.y), v2(hp.z, hp.x), L.nrm);
         } else if (kind == MAT_EMISSION) {  // shader_emission(ray, c, p, color), RM1:476-479
-            nc = v3(dm.c[0], dm.c[1], dm.c[2]) * gray_ch(v3(dm.p[0], dm.p[1], dm.p[2]) * channel_vec(L.chan), L.chan);
+            // gray_ch of p without separateChannels is a per-material constant (host, DMat.gray1)
+            float g = dm.gray1;
+            if (L.chan >= 0) g = gray_ch(v3(dm.p[0], dm.p[1], dm.p[2]) * channel_vec(L.chan), L.chan);
+            nc = v3(dm.c[0], dm.c[1], dm.c[2]) * g;
         }
         if constexpr (PROG) {  // generic node programs, one wave-uniform material at a time
             const bool valid = (kind == MAT_PROGRAM);
@@ -1360,7 +1363,11 @@ RMR_D void shade(const KParams& P, Lane& L) {
         }
         if (want) rm1_after_material<HO>(P, L, nc, nd, ni, nh);
         if (L.phase == PH_MISS) {  // shader_emission(ray, skyColor(dir), vec3(1), emit), RM1:555-561
-            const V3 emit = sky_color(P, L.d) * gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
+            // gray_ch of vec3(1) is (1 + 1 + 1) / (1 + 1 + 1) = 1 exactly without separateChannels
+            // (chan < 0): the division runs only for channel passes
+            float g = 1.0f;
+            if (L.chan >= 0) g = gray_ch(v3s(1.0f) * channel_vec(L.chan), L.chan);
+            const V3 emit = sky_color(P, L.d) * g;
             L.color = L.color * emit;
             if (finish_trace<VAR, HO>(P, L)) L.phase = PH_DONE;
         }
