@@ -688,7 +688,14 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
         sb = fminf(vlb, lbs);
     }
-    if (__ballot(!uniq)) {
+    const uint64_t amb = __ballot(!uniq);
+#ifdef RMR_NPC_AMBCOUNT   // diagnostics (RMR_JIT_OPTS=-DRMR_NPC_AMBCOUNT): fallback lanes [9], batches [10]
+    if (amb && __lane_id() == __ffsll((unsigned long long)amb) - 1) {
+        atomicAdd(P.counters + 9, (unsigned long long)__popcll(amb));
+        atomicAdd(P.counters + 10, 1ull);
+    }
+#endif
+    if (amb) {
         if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
     return d;

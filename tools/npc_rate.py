@@ -24,5 +24,7 @@ lib().rmr_get_counters(r._ctx, raw)
 print(json.dumps({"full_threshold": os.environ.get("RMR_FULL_T", "default"), "trace_ms": round(st.trace_ms, 2),
                   "map_evals": st.map_evals, "map_iters": st.map_iters, "full_batches": raw[3],
                   "lane_util": round(st.map_evals / (64.0 * st.map_iters), 4),
-                  "full_batches_per_iter": round(raw[3] / st.map_iters, 4)}))
+                  "full_batches_per_iter": round(raw[3] / st.map_iters, 4),
+                  # with RMR_JIT_OPTS=-DRMR_NPC_AMBCOUNT: lanes / batches that took the exact traversal
+                  "exact_fallback_lanes": raw[9], "exact_fallback_batches": raw[10]}))
 r.close()
