@@ -13,10 +13,19 @@ The other BASELINE configs run with --config (they are separate bench lines, not
   c5  animated Cornell-5, 1920x1080, 512 spp, 4 bounces: step f renders frame f (sphere centre
       y = 0.5 sin(2 pi f / 120)); the scene is recompiled and uploaded inside the timed step
 
-Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL). The frame's 32x32 tiles
-are dealt round-robin to the ranks; each rank renders its tiles into a zeroed full-frame
-accumulator (x + 0 = x, so the reduce is exact); frame f's reduce overlaps frame f + 1's render
-(two accumulators). Total work is fixed => "scaling": "strong".
+Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL). `--gpus N` without a
+launcher's WORLD_SIZE starts N rank processes itself (before anything in the parent touches the
+GPU); under `torch.distributed.run` the launcher's ranks are used. The frame's 32x32 tiles are dealt
+round-robin to the ranks; each rank renders its tiles into a zeroed full-frame accumulator
+(x + 0 = x, so the reduce is exact); frame f's reduce overlaps frame f + 1's render (two
+accumulators), and with N > 1 consecutive frames also overlap on two HIP streams (two renderer
+contexts), so one frame's persistent-kernel drain is filled by the next. Total work per step is
+fixed => "scaling": "strong". Rank 0's line carries the per-rank trace times and the cost of one
+frame reduce measured on its own (`multi_gpu`).
+
+`--dry-run` runs the same multi-rank schedule on the CPU (gloo, the CPU oracle as each rank's
+renderer, a 64x48 frame): rank 0 reports whether the reduced frame equals a one-process render bit
+for bit (tests/test_bench_cpu.py). It measures nothing.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
@@ -57,9 +66,12 @@ def parse():
     ap.add_argument("--kernel", type=int, default=0, help="0 persistent, 1 per-path")
     ap.add_argument("--shade-threshold", type=int, default=0)
     ap.add_argument("--traffic-json", default="")
-    ap.add_argument("--overlap", action="store_true",
-                    help="two renderer contexts on two streams: consecutive frames overlap on the GPU "
-                         "(measured +0.9%% at N=1; the per-launch event times then include waiting)")
+    ap.add_argument("--overlap", type=int, default=-1,
+                    help="1: two renderer contexts on two streams, consecutive frames overlap on the GPU "
+                         "(measured +0.9%% at N=1; the per-launch event times then include waiting); "
+                         "0: one context; default: on for N > 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
     return ap.parse_args()
 
 
@@ -153,14 +165,101 @@ def combined_stats(rs):
     return out
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N rank processes of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and return the worst exit status. The parent
+    has not imported torch or touched the GPU: the ranks are fresh processes, not exec'd."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+DRY_W, DRY_H, DRY_TILE, DRY_SPP = 64, 48, 16, 2
+
+
+def dry_run(args, cfg, rank, world):
+    """CPU rehearsal of the multi-rank schedule: gloo, the CPU oracle renders each rank's tiles
+    (test infrastructure standing in for librmr; nothing is measured), FrameRenderer's two-buffer
+    pipeline over 3 frames, one reduce per frame. Rank 0 checks every frame against a one-process
+    render of the whole frame."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from oracle import camera, oracle, scene_compile
+    from raymarchrenderer_amd import abi, time_schedule
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer, frame_tiles
+    dist_on = world > 1
+    if dist_on:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, H, T = DRY_W, DRY_H, DRY_TILE
+
+    def render_into(acc_np, tiles, times, sc):
+        t = scene_compile.load_scene_file(sc, "rm1") if isinstance(sc, str) else scene_compile.compile_scene(sc, "rm1")
+        o = oracle.Oracle(t, abi.default_params(max_bounces=cfg["bounces"]), camera.default_view(W, H), W, H)
+        for tx, ty in tiles:
+            o.render(times, rect=(tx * T, ty * T, min(W, (tx + 1) * T), min(H, (ty + 1) * T)), accum=acc_np,
+                     nthreads=2)
+
+    cur = {}
+
+    def render_fn(acc, tiles, times, first_sample):
+        a = np.zeros((H, W, 4), np.float32)
+        render_into(a, tiles, times, cur["scene"])
+        acc.copy_(torch.from_numpy(a))
+
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32) for _ in range(2)]
+    fr = FrameRenderer(None, accs, W, H, T, rank, world, dist if dist_on else None, render_fn=render_fn)
+    ok = True
+    for f in range(3):
+        cur["scene"] = scene_for_frame(cfg, f)
+        times = time_schedule(DRY_SPP, frame=f)
+        acc = fr.frame(times)
+        fr.finish()
+        if rank == 0:
+            want = np.zeros((H, W, 4), np.float32)
+            render_into(want, frame_tiles(W, H, T), times, cur["scene"])
+            ok = ok and bool(np.array_equal(acc.numpy().view(np.uint32), want.view(np.uint32)))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_ranks": world, "backend": "gloo" if dist_on else "none",
+                          "config": args.config, "frames": 3, "width": W, "height": H, "spp": DRY_SPP,
+                          "tiles_per_rank": [len(frame_tiles(W, H, T)[r::world]) for r in range(world)],
+                          "bitwise_equal_to_one_process": ok}), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
-    W, H, BOUNCES = cfg["W"], cfg["H"], cfg["bounces"]
-    spp = args.spp or cfg["spp"]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world))
+    if args.dry_run:
+        sys.exit(dry_run(args, cfg, rank, world))
+    W, H, BOUNCES = cfg["W"], cfg["H"], cfg["bounces"]
+    spp = args.spp or cfg["spp"]
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
@@ -168,10 +267,14 @@ def main():
     if dist_on:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     from raymarchrenderer_amd import Renderer, abi, time_schedule
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer, reduce_frame
+    animated = bool(cfg.get("animated"))
 
-    # --overlap: two renderer contexts on two streams; consecutive frames alternate between them,
-    # so one frame's trace-kernel drain overlaps the next frame's start (multi_gpu.FrameRenderer)
-    n_ctx = 2 if (args.overlap and not cfg.get("animated")) else 1
+    # overlap: two renderer contexts on two streams; consecutive frames alternate between them, so
+    # one frame's trace-kernel drain overlaps the next frame's start (multi_gpu.FrameRenderer).
+    # Default on for N > 1 (a rank's frame is 1/N as long, the drain is not).
+    overlap = args.overlap if args.overlap >= 0 else int(dist_on)
+    n_ctx = 2 if overlap else 1
     rs, streams = [], []
     for _ in range(n_ctx):
         r = Renderer(local_rank, W, H)
@@ -181,17 +284,24 @@ def main():
             r.set_kernel(args.kernel)
         if args.shade_threshold:
             r.set_tuning(shade_threshold=args.shade_threshold)
-        s_ = torch.cuda.Stream() if n_ctx > 1 else torch.cuda.current_stream()
+        if animated:
+            # the live-primitive kernel (rmr_jit.cpp) is built once the sphere first moves: build it
+            # here, outside every timed step, by one tiny launch of frame 1's scene
+            r.set_jit(1)
+            r.load_scene(scene_for_frame(cfg, 1), "rm1")
+            r.render_spp(time_schedule(1, frame=1), rect=(0, 0, 8, 8))
+            r.reload()
+            r.load_scene(scene_for_frame(cfg, 0), "rm1")
+        # every context on its own torch stream: FrameRenderer's zeroing, render and reduce are then
+        # ordered on that one stream (never on a private stream the collective does not wait for)
+        s_ = torch.cuda.Stream()
         r.set_stream(s_.cuda_stream)
         rs.append(r)
         streams.append(s_)
-    from raymarchrenderer_amd.multi_gpu import FrameRenderer
     n_acc = 2 if (dist_on or n_ctx > 1) else 1
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_acc)]
     torch.cuda.synchronize()
-    fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None,
-                       streams=streams if n_ctx > 1 else None)
-    animated = bool(cfg.get("animated"))
+    fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
     static_times = time_schedule(spp)
     frame_no = [0]
 
@@ -222,10 +332,33 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = combined_stats(rs)
+    per_rank = None
+    reduce_ms = None
     if dist_on:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        mine = torch.tensor([elapsed, st.trace_ms, float(st.trace_launches), float(st.map_evals),
+                             float(len(fr.tiles))], dtype=torch.float64, device="cuda")
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        allr = [a.cpu().tolist() for a in allr]
+        elapsed = max(a[0] for a in allr)
+        per_rank = [{"rank": i, "wall_ms_per_step": round(a[0] / args.steps * 1e3, 3),
+                     "trace_ms_per_step": round(a[1] / args.steps, 3),
+                     "trace_launches": int(a[2]), "map_evals": int(a[3]), "tiles32": int(a[4])}
+                    for i, a in enumerate(allr)]
+        # one frame reduce on its own (outside the timed region): what each step's collective costs
+        # when nothing overlaps it
+        acc = accs[0]
+        with torch.cuda.stream(streams[0]):
+            for _ in range(2):
+                reduce_frame(acc, dist)
+            torch.cuda.synchronize()
+            dist.barrier()
+            nrep = 5
+            t1 = time.perf_counter()
+            for _ in range(nrep):
+                reduce_frame(acc, dist)
+            torch.cuda.synchronize()
+            reduce_ms = (time.perf_counter() - t1) / nrep * 1e3
 
     samples = float(W) * H * spp * args.steps
     value = samples / elapsed / 1e6
@@ -253,6 +386,8 @@ def main():
                 "flops_per_map": st.flops_per_map,
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
                 "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
+        if n_ctx > 1:
+            roof["note"] = "overlapped frames: per-launch event times include waiting for the other stream"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -274,6 +409,11 @@ def main():
                           "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world,
                           "frame_streams": n_ctx},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity}
+        if dist_on:
+            out["multi_gpu"] = {"backend": "nccl (RCCL)", "partition": "32x32 tiles round-robin",
+                                "collective": "one reduce(SUM) of the %.1f MB RGBA32F frame per step"
+                                              % (W * H * 16 / 1e6),
+                                "reduce_ms_standalone": round(reduce_ms, 3), "per_rank": per_rank}
         print(json.dumps(out), flush=True)
     for r in rs:
         r.close()

@@ -65,7 +65,10 @@ const char* rmr_last_error(const rmr_ctx* ctx);
 /* Compile-time kernel configuration string (variants, wave size, build flags). */
 const char* rmr_build_info(void);
 
-/* Run kernels on a caller stream (a hipStream_t passed as void*; NULL = library stream). */
+/* Run kernels on a caller stream (a hipStream_t passed as void*). NULL gives the context a new
+ * library-owned non-blocking stream (it does NOT select the legacy null stream): work the caller
+ * orders on its own streams (zeroing the accumulator, a collective over it) must then be ordered
+ * with rmr_sync, so pass the caller's stream whenever it shares buffers with the renderer. */
 int rmr_set_stream(rmr_ctx* ctx, void* hip_stream);
 
 /* ---- image / view / params ------------------------------------------------------------- */
@@ -125,7 +128,8 @@ int rmr_render(rmr_ctx* ctx, float time, float min_x, float min_y, float max_x, 
 int rmr_render_spp(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1,
                    uint32_t first_sample, uint32_t nspp);
 /* Same as rmr_render_spp but over an explicit tile list (tile_size x tile_size tiles, given as
- * (tx,ty) pairs): the multi-GPU partition unit. */
+ * (tx,ty) pairs): the multi-GPU partition unit. Each (tx,ty) may appear at most once (a repeated or
+ * negative tile is RMR_E_INVALID: two threads would fold into the same pixel). */
 int rmr_render_tiles(rmr_ctx* ctx, const float* times, const int32_t* tiles_xy, int n_tiles,
                      int tile_size, uint32_t first_sample, uint32_t nspp);
 

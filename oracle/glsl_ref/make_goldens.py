@@ -42,11 +42,20 @@ IMAGES = {
     # env-map sky (useEnvTex = 1, synthetic_env): RM1:78-113 / RM2:84-107
     "rm1_sphere1_env": (os.path.join(ROOT, "scenes", "sphere1.scene"), 1, {"max_bounces": 4, "use_env_tex": 1}, 16384),
     "rm2_simple_env": (os.path.join(GS, "simple.scene"), 2, {"use_env_tex": 1}, 16384),
+    # RM1 object node set (op_union / op_subtract / op_intersect / domain_repeat / math / misc)
+    "rm1_csg_nodes_b4": (os.path.join(ROOT, "scenes", "csg_nodes.scene"), 1, {"max_bounces": 4}, 131072),
+    # C3's Mandelbulb node added to the reference path (shader_build X1), 2 bounces as C3
+    "rm1_mandelbulb_b2": (os.path.join(ROOT, "scenes", "mandelbulb.scene"), 1, {"max_bounces": 2}, 65536),
+    # C4's generator cut to 64 primitives (the reference codegen compiles it; 256 does not finish)
+    "rm1_csg64_b4": (os.path.join(ROOT, "scenes", "csg64.scene"), 1, {"max_bounces": 4}, 32768),
 }
 KATS = {
     "rm3": (None, 3),
     "cornell5": (os.path.join(ROOT, "scenes", "cornell5.scene"), 1),
     "default": (os.path.join(GS, "default.scene"), 1),
+    "csg_nodes": (os.path.join(ROOT, "scenes", "csg_nodes.scene"), 1),
+    "mandelbulb": (os.path.join(ROOT, "scenes", "mandelbulb.scene"), 1),
+    "csg64": (os.path.join(ROOT, "scenes", "csg64.scene"), 1),
 }
 
 
@@ -149,7 +158,7 @@ def make_image(name, path, variant, kw, conv_spp, threads):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="")
+    ap.add_argument("--only", default="", help="comma-separated fixture names (kat_<scene>, kat_nan, <image>)")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--conv-scale", type=float, default=1.0)
     args = ap.parse_args()
@@ -171,17 +180,17 @@ def main():
     man.setdefault("images", {})
     rng = np.random.default_rng(20251015)
     for name, (path, variant) in KATS.items():
-        if args.only and args.only != "kat_" + name:
+        if args.only and "kat_" + name not in args.only.split(","):
             continue
         make_kat(name, path, variant, rng)
         man["kat"][name] = {"scene": os.path.relpath(path, ROOT) if path else "builtin", "variant": variant}
         print("kat", name, flush=True)
-    if not args.only or args.only == "kat_nan":
+    if not args.only or "kat_nan" in args.only.split(","):
         make_kat_nan(np.random.default_rng(7))
         man["kat"]["nan"] = {"scenes": [k for k, v in KATS.items() if v[1] == 1], "probe": "map/march with NaN dir"}
         print("kat nan", flush=True)
     for name, (path, variant, kw, spp) in IMAGES.items():
-        if args.only and args.only != name:
+        if args.only and name not in args.only.split(","):
             continue
         spp = int(spp * args.conv_scale)
         dt = make_image(name, path, variant, kw, spp, args.threads)

@@ -11,6 +11,11 @@ RayMarch2.glsl's mat_func_1). Patches needed to compile/run on Mesa llvmpipe (SU
   P3  zero-initialise generated out params / locals (`out` params are undefined on entry; rmr
       defines them as vec3(0))
   P4  (probe shaders only) main() renamed ref_main(); a KAT main() appended.
+  X1  scenes with a map_mandelbulb node (not in the reference's node set) get the
+      builder's GLSL statement of that node (EXT_MANDELBULB below, written for this harness, not
+      taken from the reference) inserted with the object functions, in the reference's node ABI
+      (vec3 in/out). It uses the driver's own pow/acos/atan/sin/cos/log, so the C3 fixture is
+      "the reference path with that node added" (SURVEY §8d), pinned by PSNR like the others.
 """
 import json
 import os
@@ -159,6 +164,39 @@ def v2_materials(materials):
     return lines
 
 
+# X1: the Mandelbulb distance estimator as a v1 object node (same statement as rmr's sd_mandelbulb:
+# csrc/rmr_trace.h; inputs P, centre, (power, iterations, bailout))
+EXT_MANDELBULB = r"""
+void map_mandelbulb(in vec3 p, in vec3 centre, in vec3 prm, out vec3 d)
+{
+	vec3 p0 = p - centre;
+	vec3 z = p0;
+	float power = prm.x;
+	float bail = prm.z;
+	int iters = int(prm.y);
+	float dr = 1.0;
+	float r = 0.0;
+	for (int i = 0; i < iters; i++)
+	{
+		r = length(z);
+		if (r > bail) break;
+		float theta = acos(z.z / r);
+		float phi = atan(z.y, z.x);
+		dr = pow(r, power - 1.0) * power * dr + 1.0;
+		float zr = pow(r, power);
+		theta = theta * power;
+		phi = phi * power;
+		z = vec3(sin(theta) * cos(phi), sin(phi) * sin(theta), cos(theta)) * zr + p0;
+	}
+	d = vec3(0.5 * log(r) * r / dr);
+}  // (not a bare "}": expand() counts objects by those lines)
+"""
+
+
+def _uses(objects, name):
+    return any(n.get("name") == name for o in objects for n in o.get("nodes", []))
+
+
 def expand(src_lines, mat_lines, obj_lines, objects):
     """Graphics::loadShader marker expansion, Graphics.cpp:60-113."""
     lines = list(src_lines)
@@ -216,6 +254,8 @@ def build(variant, scene=None, probe_main=None):
     if variant == 1:
         mat_lines = v1_materials(scene.get("materials", []))
         obj_lines = v1_objects(scene.get("objects", []))
+        if _uses(scene.get("objects", []), "map_mandelbulb"):   # X1 (not a reference node)
+            obj_lines = EXT_MANDELBULB.strip("\n").split("\n") + obj_lines
     elif variant == 2:
         mat_lines = v2_materials(scene.get("materials", []))
         obj_lines = []

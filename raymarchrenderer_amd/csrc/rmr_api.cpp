@@ -332,8 +332,17 @@ int ensure_jit(rmr_ctx* c) {
     }
     rmr::JitKernel k;
     k.key = key;
-    HIPCHK(c, hipModuleLoadData(&k.module, code.data()));
-    HIPCHK(c, hipModuleGetFunction(&k.fn, k.module, "rmr_jit_trace"));
+    // a code object that does not load (e.g. a stale disk-cache entry) marks the scene as failed, so
+    // auto mode falls back to the ahead-of-time kernels instead of retrying every launch
+    if (hipModuleLoadData(&k.module, code.data()) != hipSuccess) {
+        c->jit_failed = true;
+        return fail(c, RMR_E_HIP, "hipModuleLoadData of the specialised kernel failed (key " + key + ")");
+    }
+    if (hipModuleGetFunction(&k.fn, k.module, "rmr_jit_trace") != hipSuccess) {
+        (void)hipModuleUnload(k.module);
+        c->jit_failed = true;
+        return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
+    }
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, 256, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
@@ -897,6 +906,17 @@ int rmr_render_tiles(rmr_ctx* c, const float* times, const int32_t* tiles_xy, in
                      uint32_t first_sample, uint32_t nspp) {
     if (!c || (!times && nspp) || (!tiles_xy && n_tiles) || tile_size <= 0 || (tile_size % 8) != 0)
         return fail(c, RMR_E_INVALID, "tile_size must be a positive multiple of 8");
+    // every (tx, ty) at most once: k_fold gives each pixel of a launch one thread, and a repeated
+    // tile would have two threads read-modify-write the same accumulator pixel
+    std::vector<std::pair<int, int>> seen;
+    seen.reserve((size_t)n_tiles);
+    for (int i = 0; i < n_tiles; i++) {
+        if (tiles_xy[2 * i] < 0 || tiles_xy[2 * i + 1] < 0) return fail(c, RMR_E_INVALID, "negative tile index");
+        seen.emplace_back(tiles_xy[2 * i], tiles_xy[2 * i + 1]);
+    }
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end())
+        return fail(c, RMR_E_INVALID, "duplicate tile in rmr_render_tiles");
     std::vector<TileXY> t;
     t.reserve((size_t)n_tiles * (tile_size / 8) * (tile_size / 8));
     for (int i = 0; i < n_tiles; i++) {

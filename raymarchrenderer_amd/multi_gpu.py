@@ -48,7 +48,11 @@ class FrameRenderer:
 
     `accums`: one torch tensor (H x W x 4 float32) or a list of two for the pipelined schedule.
     `renderer`: a raymarchrenderer_amd.Renderer (the accumulator is bound with rmr_bind_accum), or
-    None with `render_fn(acc, tiles, times, first_sample)` (tests: the CPU oracle under gloo)."""
+    None with `render_fn(acc, tiles, times, first_sample)` (tests: the CPU oracle under gloo).
+    `streams`: one torch.cuda.Stream per renderer. Without them each renderer gets a new torch
+    stream here (rmr_set_stream): a frame's zeroing, its render and the collective that reads it
+    must be ordered on one stream the collective waits for — a renderer left on its library-owned
+    non-blocking stream would race both."""
 
     def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
@@ -56,6 +60,11 @@ class FrameRenderer:
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
         if len(self.accs) % len(self.rs):
             raise ValueError("accumulators must be a multiple of the renderers")
+        if streams is None and render_fn is None:
+            import torch
+            streams = [torch.cuda.Stream() for _ in self.rs]
+            for r, s in zip(self.rs, streams):
+                r.set_stream(s.cuda_stream)
         self.streams = list(streams) if streams is not None else None
         self.work = [None] * len(self.accs)
         self.tiles = tile_partition(W, H, tile, rank, world)

@@ -1,0 +1,41 @@
+"""bench.py's multi-rank launch on the CPU: `--gpus N` without a launcher starts N rank processes
+(RANK / WORLD_SIZE / MASTER_* on 127.0.0.1) and `--dry-run` runs the frame schedule over gloo with the
+CPU oracle as each rank's renderer. Rank 0's frames must equal a one-process render bit for bit
+(the tile partition + one reduce per frame is exact). Nothing here touches a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(args), capture_output=True,
+                       text=True, timeout=600, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout      # one JSON line, from rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("gpus,config", [(2, "c2"), (3, "c5")])
+def test_bench_spawns_ranks_and_reduces_exactly(gpus, config):
+    out = _run("--gpus", str(gpus), "--dry-run", "--config", config)
+    assert out["dry_run"] is True
+    assert out["n_ranks"] == gpus and out["backend"] == "gloo"
+    assert out["bitwise_equal_to_one_process"] is True
+    assert sum(out["tiles_per_rank"]) == (64 // 16) * (48 // 16)
+
+
+def test_bench_rejects_mismatched_launcher():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "--gpus 2" in p.stderr

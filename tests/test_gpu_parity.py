@@ -44,6 +44,11 @@ CASES = [
     ("rm2_simple_sepch", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"separate_channels": 1}),
     # separateChannels on the HO fast kernel (escape bound + approximate map per channel trace)
     ("rm1_cornell5_sepch", os.path.join(SCENES, "cornell5.scene"), "rm1", {"separate_channels": 1, "max_bounces": 4}),
+    # RM1's object node set (op_union / op_subtract / op_intersect / domain_repeat / math / misc,
+    # RayMarch.glsl:121-215) through the node interpreter; the 64-primitive cut of C4's generator
+    # through the BVH + nearest-primitive cache
+    ("rm1_csg_nodes_b4", os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}),
+    ("rm1_csg64_b4", os.path.join(SCENES, "csg64.scene"), "rm1", {"max_bounces": 4}),
 ]
 
 

@@ -24,6 +24,8 @@ SCENE_CASES = [
     ("rm2_simple", os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {}),
     ("rm3_builtin", None, "rm3", {}),
     ("rm1_sphere1_env", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
+    ("rm1_csg_nodes_b4", os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}),
+    ("rm1_csg64_b4", os.path.join(SCENES, "csg64.scene"), "rm1", {"max_bounces": 4}),
 ]
 IDS = [c[0] for c in SCENE_CASES]
 

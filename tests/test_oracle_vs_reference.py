@@ -16,11 +16,26 @@ from raymarchrenderer_amd import abi, parity_schedule, time_schedule
 from .conftest import GOLDEN, SCENES
 
 KATS = {"rm3": (None, "rm3"), "cornell5": (os.path.join(SCENES, "cornell5.scene"), "rm1"),
-        "default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1")}
+        "default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1"),
+        # RM1's object node set: op_union / op_subtract / op_intersect / domain_repeat / math / misc
+        "csg_nodes": (os.path.join(SCENES, "csg_nodes.scene"), "rm1"),
+        # C3's Mandelbulb node added to the reference path (oracle/glsl_ref/shader_build.py X1)
+        "mandelbulb": (os.path.join(SCENES, "mandelbulb.scene"), "rm1"),
+        # C4's generator cut to 64 primitives (the BVH / nearest-primitive-cache scene size class)
+        "csg64": (os.path.join(SCENES, "csg64.scene"), "rm1")}
 
 
 def _tables(path, variant):
     return scene_compile.compile_scene({}, variant) if path is None else scene_compile.load_scene_file(path, variant)
+
+
+# The Mandelbulb's distance estimator iterates pow / acos / atan / sin / cos / log of the driver
+# (llvmpipe) against the oracle's deterministic ones (oracle/detmath.h): GLSL leaves their precision
+# to the implementation, and the fractal iteration amplifies ulp-level differences (measured: map
+# within 3e-5 relative, march within 1e-4, normals — central differences with h = 0.001 of that
+# distance — median 1e-6, worst 0.04 of 104). Its tolerances say so; every other scene is held to
+# float rounding.
+MAP_RTOL = {"mandelbulb": 1e-4}
 
 
 @pytest.mark.parametrize("name", sorted(KATS))
@@ -29,7 +44,7 @@ def test_kat_map(name):
     t = _tables(*KATS[name])
     out = np.array([oracle.map_p(t, p) for p in k["map_in"]])
     ref = k["map_out"]
-    assert np.all(np.abs(out[:, 0] - ref[:, 0]) <= 2e-6 * np.maximum(1.0, np.abs(ref[:, 0])))
+    assert np.all(np.abs(out[:, 0] - ref[:, 0]) <= MAP_RTOL.get(name, 2e-6) * np.maximum(1.0, np.abs(ref[:, 0])))
     assert np.array_equal(out[:, 1], ref[:, 1])
 
 
@@ -50,7 +65,11 @@ def test_kat_normal(name):
     t = _tables(*KATS[name])
     hit = k["march_out"][:, 0] < 1000
     out = np.array([oracle.normal(t, p) for p in k["normal_in"][hit]])
-    assert np.abs(out - k["normal_out"][hit]).max() <= 1e-4
+    err = np.abs(out - k["normal_out"][hit]).max(axis=1)
+    if name == "mandelbulb":   # see MAP_RTOL
+        assert np.median(err) <= 1e-4 and np.percentile(err, 90) <= 5e-3 and err.max() <= 0.1
+    else:
+        assert err.max() <= 1e-4
 
 
 @pytest.mark.parametrize("name", ["cornell5", "default"])
