@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-psnr", action="store_true", help="skip the converged PSNR check vs the reference render")
+    ap.add_argument("--no-count-pass", action="store_true",
+                    help="skip the executed-work count pass (roofline flops then use the static per-map count)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel", type=int, default=0, help="0 persistent, 1 per-path")
     ap.add_argument("--shade-threshold", type=int, default=0)
@@ -111,9 +113,34 @@ def cpu_baseline(cfg, spp, seconds, threads):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d samples: rows y%%%d==0 of the %dx%d frame, 1 spp per row pass, %d-thread OpenMP C "
-                      "restatement (oracle/rmr_oracle.c)" % (done, stride, W, H, threads)}
+    out = {"value": done / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": "%d samples: rows y%%%d==0 of the %dx%d frame, 1 spp per row pass, %d-thread OpenMP C "
+                     "restatement (oracle/rmr_oracle.c); %d threads = the host-CPU share of one GPU on "
+                     "this box (OMP_NUM_THREADS)" % (done, stride, W, H, threads, threads)}
+    ref = LLVMPIPE_PER_VCPU.get(cfg_name_of(cfg))
+    if ref:
+        # the reference's own path (RayMarch.glsl on Mesa llvmpipe) cannot run on the GPU box (no
+        # reference sources there): its per-vCPU rate measured in the build container (BASELINE.md
+        # §2, 8 vCPU), scaled to the same core count, beside the port's measured rate
+        out["reference_llvmpipe_scaled"] = {
+            "value": round(ref[0] * threads, 3), "per_vcpu": ref[0], "cores": threads,
+            "basis": ref[1] + "; scaled linearly to %d cores, not measured on this box" % threads}
+    return out
+
+
+# Msamples/s per vCPU of the reference GLSL on llvmpipe (BASELINE.md §2 / SURVEY §6, 8 vCPU Xeon)
+LLVMPIPE_PER_VCPU = {
+    "c1": (3.65 / 8, "RM1 single sphere 256x256 1 spp: 3.5-3.8 Msamples/s on 8 vCPU"),
+    "c2": (3.56 / 8, "RM1 Cornell-5 1920x1080 4 bounces: 3.56 Msamples/s on 8 vCPU"),
+    "c5": (3.56 / 8, "RM1 Cornell-5 (C5's scene, static) 1920x1080 4 bounces: 3.56 Msamples/s on 8 vCPU"),
+}
+
+
+def cfg_name_of(cfg):
+    for k, v in CONFIGS.items():
+        if v is cfg:
+            return k
+    return None
 
 
 GOLDEN_OF = {"c1": "img_rm1_sphere1_b1.npz", "c2": "img_rm1_cornell5_b4.npz"}
@@ -148,6 +175,44 @@ def psnr_vs_reference(cfg_name, cfg, device):
     return {"psnr_db": round(float(psnr), 2), "mean_rel_diff": round(float(rel), 5),
             "reference": "RayMarch.glsl on Mesa llvmpipe, %dx%d, %d spp (tests/golden/%s)" % (W, H, n, name),
             "gpu_spp": n}
+
+
+def count_pass(cfg, spp, device, n_count=8):
+    """Executed SDF work of the workload, measured by the counting build of the specialised kernel
+    (rmr_trace.h RMR_COUNT_FLOPS: a separate code object; same control flow and results, one atomic
+    per wave and counted event, so it is timed nowhere). Runs the first n_count samples of the same
+    frame (all tiles) outside the timed region; samples are identically distributed, so the per-map
+    ratios hold for the whole frame. Returns per-map executed flops, transcendentals and the
+    Mandelbulb-iteration share."""
+    import ctypes as C
+    from raymarchrenderer_amd import Renderer, abi, lib, time_schedule
+    from raymarchrenderer_amd.multi_gpu import frame_tiles
+    W, H = cfg["W"], cfg["H"]
+    n = min(spp, n_count)
+    old = os.environ.get("RMR_JIT_OPTS")
+    os.environ["RMR_JIT_OPTS"] = ((old + " ") if old else "") + "-DRMR_COUNT_FLOPS"
+    r = Renderer(device, W, H)
+    try:
+        r.set_jit(1)
+        r.load_scene(scene_for_frame(cfg, 0), "rm1")
+        r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
+        r.reset_stats()
+        r.render_tiles(time_schedule(n), frame_tiles(W, H, TILE), TILE)
+        r.sync()
+        cnt = (C.c_uint64 * 16)()
+        lib().rmr_get_counters(r.ctx, cnt)
+        st = r.stats()
+    finally:
+        r.close()
+        if old is None:
+            os.environ.pop("RMR_JIT_OPTS", None)
+        else:
+            os.environ["RMR_JIT_OPTS"] = old
+    maps = float(cnt[0])
+    return {"samples": "first %d of %d samples of the frame, all tiles" % (n, spp), "map_evals": int(cnt[0]),
+            "flops_per_map": cnt[11] / maps, "transc_per_map": cnt[12] / maps,
+            "mandelbulb_flops_per_map": cnt[13] / maps, "static_flops_per_map": st.flops_per_map,
+            "launches": int(st.trace_launches)}
 
 
 class _Stats:
@@ -365,11 +430,22 @@ def main():
     ms_step = elapsed / args.steps * 1e3
 
     roof = None
+    cp = None
+    if rank == 0 and not args.no_count_pass and st.jit_launches:
+        cp = count_pass(cfg, spp, local_rank)
     if st.trace_launches > 0 and st.trace_ms > 0:
-        # rank 0's dominant kernel: its own map evals over its own launches
+        # rank 0's dominant kernel: its own map evals over its own launches. Executed flops per map
+        # from the count pass (BVH / cache maps evaluate a few primitives, the Mandelbulb iterates a
+        # point-dependent number of times); reference-equivalent: every primitive of the scene per
+        # map, as the reference's map() evaluates them (RM1:224-231)
         per_launch_ms = st.trace_ms / st.trace_launches
-        flops_per_launch = float(st.map_evals) / st.trace_launches * st.flops_per_map
-        achieved = flops_per_launch / (per_launch_ms * 1e-3) / 1e12
+        maps_per_launch = float(st.map_evals) / st.trace_launches
+        if cp is not None:
+            fpm = cp["flops_per_map"]
+            ref_fpm = st.flops_per_map + cp["mandelbulb_flops_per_map"]
+        else:
+            fpm = ref_fpm = st.flops_per_map
+        achieved = maps_per_launch * fpm / (per_launch_ms * 1e-3) / 1e12
         traffic = None
         tj = args.traffic_json or os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
         if os.path.exists(tj) and world == 1 and spp == cfg["spp"]:
@@ -383,7 +459,12 @@ def main():
                 "kernel": ("rmr_jit_trace (hipRTC scene-specialised trace kernel)" if st.jit_launches
                            else "k_trace<RM1,persistent>"), "avg_launch_ms": round(per_launch_ms, 3),
                 "map_evals_per_launch": int(st.map_evals / st.trace_launches),
-                "flops_per_map": st.flops_per_map,
+                "flops_per_map": round(fpm, 2),
+                "flops_basis": ("executed (count pass: %s)" % cp["samples"]) if cp else "static per-map count",
+                "ref_equiv_flops_per_map": round(ref_fpm, 2),
+                "ref_equiv_achieved": round(maps_per_launch * ref_fpm / (per_launch_ms * 1e-3) / 1e12, 3),
+                "transcendentals_per_s": (round(maps_per_launch * cp["transc_per_map"] / (per_launch_ms * 1e-3), 1)
+                                          if cp else None),
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
                 "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
         if n_ctx > 1:

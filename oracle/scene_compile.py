@@ -422,10 +422,12 @@ def load_scene_file(path, variant):
 
 
 def flops_per_map(t):
-    """Algorithmic flops of one map(): sphere 10, box 22, opU 2 per prim after the first."""
+    """Algorithmic flops of one map() (SURVEY §8d): sphere 10, box 22, opU 2 per prim after the first;
+    a Mandelbulb's fixed part 6 (its iterations are counted at run time, csrc/scene.cpp)."""
     f = 0
     for p in t.prims:
-        f += {abi.RMR_PRIM_SPHERE: 10, abi.RMR_PRIM_BOX: 22}.get(p.type, 10 * max(1, p.prog_end - p.prog_begin))
+        f += {abi.RMR_PRIM_SPHERE: 10, abi.RMR_PRIM_BOX: 22, abi.RMR_PRIM_MANDELBULB: 6}.get(
+            p.type, 10 * max(1, p.prog_end - p.prog_begin))
     return f + 2 * max(0, len(t.prims) - 1)
 
 

@@ -631,6 +631,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.accum = c->d_accum;
     P.queue = c->d_queue;
     P.counters = c->d_counters;
+    P.flops_static = (int32_t)s.flops_per_map();
+    P.transc_static = (int32_t)s.transc_per_map();
     P.shade_threshold = c->shade_threshold;
     P.refill_threshold = c->refill_threshold > 0 ? c->refill_threshold : c->shade_threshold;
 

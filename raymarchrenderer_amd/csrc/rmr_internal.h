@@ -94,6 +94,8 @@ struct KParams {
     float4* accum;              // W*H running mean
     unsigned long long* queue;  // persistent work counter
     unsigned long long* counters; // [0] map evals, [1] samples traced
+    int32_t flops_static;       // count builds (RMR_COUNT_FLOPS): flops of one map() fold without the
+    int32_t transc_static;      //   Mandelbulb iterations, and its transcendentals (scene.cpp)
     int32_t shade_threshold;    // deferred-shading batch size (lanes)
     int32_t refill_threshold;   // idle lanes before a wave fetches new units
 };

@@ -92,6 +92,33 @@ template <bool HO> RMR_D const V3& hitref(const Lane& L) {
 template <int VAR, bool PROG> constexpr bool hit_in_origin() { return VAR != RMR_VARIANT_RM2 && !PROG; }
 
 // ------------------------------------------------------------------------------------------
+// Executed-work counting (roofline, bench.py's count pass). Only kernels built with
+// -DRMR_COUNT_FLOPS count (the hipRTC kernel with RMR_JIT_OPTS=-DRMR_COUNT_FLOPS, a separate code
+// object): P.counters[11] += algorithmic flops of the SDF evaluations the kernel actually performed
+// (SURVEY §8d prices: box 22, sphere 10, opU fold 2; Mandelbulb per call 6 + per iteration 27),
+// [12] += their transcendentals (sqrt, acos, atan2, log, exp, sin, cos: 1 per sphere/box, Mandelbulb
+// 1 per call + 10 per iteration), [13] += the Mandelbulb iteration flops alone. Lane-level sums, one
+// atomic per wave and event, so the counting kernel is slower; it computes the same bits.
+// ------------------------------------------------------------------------------------------
+#ifdef RMR_COUNT_FLOPS
+RMR_D void count_work(unsigned long long* cnt, uint64_t lanes, uint64_t flops_per_lane, uint64_t transc_per_lane,
+                      uint64_t mb_flops_per_lane = 0) {
+    const uint64_t m = __ballot(1);
+    if (cnt && lanes && __lane_id() == __ffsll((unsigned long long)m) - 1) {
+        atomicAdd(cnt + 11, (unsigned long long)(lanes * flops_per_lane));
+        if (transc_per_lane) atomicAdd(cnt + 12, (unsigned long long)(lanes * transc_per_lane));
+        if (mb_flops_per_lane) atomicAdd(cnt + 13, (unsigned long long)(lanes * mb_flops_per_lane));
+    }
+}
+#define RMR_COUNT(cnt, lanes, f, t) count_work((cnt), (lanes), (f), (t))
+#define RMR_COUNT_MB(cnt, lanes) count_work((cnt), (lanes), 27, 10, 27)
+#else
+#define RMR_COUNT(cnt, lanes, f, t) ((void)0)
+#define RMR_COUNT_MB(cnt, lanes) ((void)0)
+#endif
+RMR_D uint64_t active_lanes() { return (uint64_t)__popcll(__ballot(1)); }
+
+// ------------------------------------------------------------------------------------------
 // RNG: rand(co), RM1:44-57 (chained fract(sin) hash, state randChange per invocation)
 // ------------------------------------------------------------------------------------------
 RMR_D float rand_step(float gxt, float gyt, float& rc, V2 co) {
@@ -141,14 +168,17 @@ RMR_D float sd_box(V3 p, V3 c, V3 r) {                                          
 #else
 #define RMR_MB_ATTR __device__ __noinline__
 #endif
-RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm) {
+// cnt: the count build's counters (P.counters), nullptr where the caller has none
+RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nullptr) {
     V3 p0 = p - c, z = p0;
     float power = prm.x, bail = prm.z;
     int iters = (int)prm.y;
     float dr = 1.0f, r = 0.0f;
+    (void)cnt;
     for (int i = 0; i < iters; i++) {
         r = length(z);
         if (r > bail) break;
+        RMR_COUNT_MB(cnt, active_lanes());   // one iteration of the lanes still iterating
         float theta = det_acos(z.z / r);
         float phi = det_atan2(z.y, z.x);
         // det_pow(r, power - 1) and det_pow(r, power) with their shared det_log(r) computed once,
@@ -434,7 +464,7 @@ RMR_D V2 map_general(const KParams& P, V3 p) {
         float dj;
         if (type == RMR_PRIM_BOX) dj = sd_box(p, c, r);
         else if (type == RMR_PRIM_SPHERE) dj = sd_sphere(p, c, r.x);
-        else if (type == RMR_PRIM_MANDELBULB) dj = sd_mandelbulb(p, c, r);
+        else if (type == RMR_PRIM_MANDELBULB) dj = sd_mandelbulb(p, c, r, P.counters);
         else dj = obj_program(P, pr[j].prog_begin, pr[j].prog_end, pr[j].dist_var, p);
         opu(d, dj, pr[j].mat_id);
     }
@@ -477,6 +507,7 @@ RMR_D V2 map_bvh(const KParams& P, V3 p) {
             const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
             const float mid = pr[k].mat_id;
             const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
+            RMR_COUNT(P.counters, active_lanes(), (type == RMR_PRIM_BOX ? 22 : 10) + 2, 1);
             if (dj < dbest || (dj == dbest && j > jbest)) { dbest = dj; mbest = mid; jbest = j; }
             if (dj != dj && j > jnan) { jnan = j; mnan = mid; }
         }
@@ -533,7 +564,9 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
 // Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id ms;
 // ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
 // distance tightens the culling bound from the first node on.
-RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
+                           bool count = true) {
+    (void)count;
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
     CDPrim* pr = (CDPrim*)P.dprims;
@@ -574,6 +607,7 @@ RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb,
             const float mid = pr[k].mat_id;
             if (k == ks) continue;   // the seed, already folded in
             const float dj = (type == RMR_PRIM_BOX) ? sd_box(p, c, r) : sd_sphere(p, c, r.x);
+            if (count) RMR_COUNT(P.counters, active_lanes(), (type == RMR_PRIM_BOX ? 22 : 10) + 2, 1);
             // insert dj into (u1, u2, u3): u3' = med3(u2, dj, u3), u2' = med3(u1, dj, u2), u1' = min
             const bool lt1 = dj < u1, lt2 = dj < u2;
             u3 = __builtin_amdgcn_fmed3f(u2, dj, u3);
@@ -660,6 +694,7 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
             const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
             if (k == ks) continue;
             const float a = am_prim(type, p, c, r);
+            RMR_COUNT(P.counters, active_lanes(), (type == RMR_PRIM_BOX ? 22 : 10) + 2, 1);
             const bool lt1 = a < u1, lt2 = a < u2;
             u3 = __builtin_amdgcn_fmed3f(u2, a, u3);
             u2 = __builtin_amdgcn_fmed3f(u1, a, u2);
@@ -696,7 +731,7 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
     }
 #endif
     if (amb) {
-        if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
+        if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);   // (re-evaluation: not counted)
     }
     return d;
 }
@@ -705,6 +740,8 @@ template <int NP>
 struct TableMap {
     // NP == -3: the BVH map with the nearest-primitive cache (trace_main's kCache path)
     static constexpr bool kCache = (NP == -3);
+    // the map counts its own executed work (BVH traversals skip primitives; see RMR_COUNT_FLOPS)
+    static constexpr bool kCounts = (NP == -2 || NP == -3);
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
@@ -1609,6 +1646,17 @@ RMR_D void trace_main(const KParams& P) {
                     } else {
                         opu(m, F, mid);
                     }
+#ifdef RMR_COUNT_FLOPS
+                    {   // the cached primitives evaluated here (types per lane: the leaf table's)
+                        const int t1 = __float_as_int(((const float4*)(P.dprims + L.cw))[1].z) & 0xff;
+                        const int t2 = __float_as_int(((const float4*)(P.dprims + L.cw2))[1].z) & 0xff;
+                        const uint64_t nb = (uint64_t)__popcll(__ballot(t1 == RMR_PRIM_BOX)) +
+                                            (RMR_NPC_K >= 2 ? (uint64_t)__popcll(__ballot(t2 == RMR_PRIM_BOX)) : 0);
+                        const uint64_t n = active_lanes() * (RMR_NPC_K >= 2 ? 2 : 1);
+                        RMR_COUNT(P.counters, n - nb, 10 + 2, 1);
+                        RMR_COUNT(P.counters, nb, 22 + 2, 1);
+                    }
+#endif
                     const float delta = (L.phase == PH_NORMAL) ? NPC_PROBE_DELTA : (L.t - L.cta) * (1.0f + 0x1p-21f);
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
                     ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > Fm);
@@ -1651,6 +1699,8 @@ RMR_D void trace_main(const KParams& P) {
             for (;;) {
                 if (is_active(L.phase)) {
                     const V3 p = RMR_MARCH_POINT(L);
+                    if constexpr (!MAP::kCounts)   // every primitive of the fold (Mandelbulb iterations: inside)
+                        RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
                     const V2 m = MAP::eval(P, p);
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO>(P, L, m);

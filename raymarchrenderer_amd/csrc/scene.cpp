@@ -418,15 +418,27 @@ float max_sphere_radius(const CompiledScene& s) {
     return r;
 }
 
+// Algorithmic flops of one map() (add/sub/mul/min/max/abs/compare 1, FMA 2, sqrt 1 (+1
+// transcendental), division 1): sphere 10, box 22, opU fold 2 per primitive after the first, a node
+// program ~10 per node. A Mandelbulb primitive's fixed part is 6 (p - c; 0.5 log(r) r / dr); its
+// iterations — 27 flops and 10 transcendentals each (length 6, bailout test 1, z.z / r 1, log-guard
+// tests 2, power - 1 1, two exponent products 2, dr fma 3, angle scaling 2, direction products 2,
+// z = dir zr + p0 6; sqrt, acos, atan2, log, exp x2, sin x2, cos x2) — depend on the point and are
+// counted at run time by the RMR_COUNT_FLOPS build (rmr_trace.h).
 double CompiledScene::flops_per_map() const {
     double f = 0;
     for (const auto& p : prims) {
         if (p.type == RMR_PRIM_SPHERE) f += 10;
         else if (p.type == RMR_PRIM_BOX) f += 22;
-        else if (p.type == RMR_PRIM_MANDELBULB) f += 45.0 * p.r[1];
+        else if (p.type == RMR_PRIM_MANDELBULB) f += 6;
         else f += 10.0 * std::max(1, p.prog_end - p.prog_begin);
     }
     return f + 2.0 * std::max<double>(0, (double)prims.size() - 1);
+}
+double CompiledScene::transc_per_map() const {
+    double t = 0;
+    for (const auto& p : prims) t += (p.type == RMR_PRIM_PROGRAM) ? 0.0 : 1.0;
+    return t;
 }
 
 CompiledScene compile_scene(const std::string& text, int variant) {

@@ -26,7 +26,8 @@ struct CompiledScene {
 
     rmr_scene view() const;                           // non-owning rmr_scene over the vectors
     void from_tables(const rmr_scene& s);             // deep copy
-    double flops_per_map() const;                     // SURVEY §8d counting convention
+    double flops_per_map() const;
+    double transc_per_map() const;                     // SURVEY §8d counting convention
 };
 
 // JSON text -> tables for `variant`; throws SceneError with the reason the reference's generated

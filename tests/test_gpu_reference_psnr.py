@@ -34,6 +34,8 @@ CASES = {
     "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}, 40.0),
     "rm1_sphere1_env": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}, 40.0),
     "rm2_simple_env": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}, 40.0),
+    # round 2: RM1's object node set (op_* / domain_repeat / math / misc)
+    "rm1_csg_nodes_b4": (os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}, 40.0),
 }
 
 

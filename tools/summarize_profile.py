@@ -1,10 +1,10 @@
 """Summarise a tools/profile_round.sh run (gpurun_out/{prof,pmcf,pmcw,pmcs,pmcv}_<tag>) into profiles/.
 
-    python tools/summarize_profile.py r01
+    python tools/summarize_profile.py r01 [CONFIG]     (CONFIG: bench.py --config, default c2)
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats of the bench command, verbatim),
 profiles/<tag>_pmc.json (per-launch PMC values of the dominant kernel and derived ratios) and
-profiles/traffic_c2.json (HBM bytes per k_trace launch, read by bench.py for roofline.traffic).
+profiles/traffic_<config>.json (HBM bytes per k_trace launch, read by bench.py for roofline.traffic).
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide streaming reads, so it is
@@ -35,7 +35,7 @@ def counters(d, match):
     return {k: sum(v) / len(v) for k, v in agg.items()}, meta
 
 
-def main(tag):
+def main(tag, config="c2"):
     os.makedirs(PROF, exist_ok=True)
     shutil.copy(os.path.join(GO, "prof_%s" % tag, "run_kernel_stats.csv"),
                 os.path.join(PROF, "%s_kernel_stats.csv" % tag))
@@ -44,7 +44,8 @@ def main(tag):
     match = "rmr_jit_trace" if any("rmr_jit_trace" in n for n in stats) else "k_trace"
     trace = [r for n, r in stats.items() if match in n][0]
     out = {"tag": tag, "kernel_name": trace["Name"],
-           "command": "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline (C2 1920x1080, 64 spp)",
+           "command": "python3 bench.py --config %s --no-cpu-baseline --no-psnr --no-count-pass "
+                      "(tools/profile_round.sh)" % config,
            "k_trace_avg_ns": float(trace["AverageNs"]), "k_trace_calls": int(trace["Calls"])}
     c = {}
     meta = {}
@@ -74,7 +75,7 @@ def main(tag):
     }
     with open(os.path.join(PROF, "%s_pmc.json" % tag), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    with open(os.path.join(PROF, "traffic_c2.json"), "w") as f:
+    with open(os.path.join(PROF, "traffic_%s.json" % config), "w") as f:
         json.dump({"tag": tag, "hbm_bytes_per_launch": round(hbm), "fetch_bytes_x2": round(2 * fetch),
                    "write_bytes": round(write),
                    "note": "FETCH_SIZE x2 + WRITE_SIZE (KiB->B) per k_trace launch; see %s_pmc.json" % tag},
@@ -83,4 +84,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "c2")
