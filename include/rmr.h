@@ -168,6 +168,24 @@ int rmr_set_kernel(rmr_ctx* ctx, int kernel);
  * direction +y). Used when params.use_env_tex != 0; NULL removes it. Sampling: bilinear, level 0,
  * CLAMP_TO_EDGE. */
 int rmr_set_env_map(rmr_ctx* ctx, const uint8_t* rgba8, int w, int h);
+
+/* ---- display ---------------------------------------------------------------------------- */
+/* Graphics::Display(centre, zoom, min, max) (Graphics.cpp:356-390 with createFQ 227-258 and
+ * FullQuad.vs / FullQuad.fs), headless: draws the accumulator into a screen_w x screen_h RGBA8 image
+ * (row 0 = top, the window's coordinates; Screen::getScreenSize() is the image size) the way the
+ * reference's textured quad does: quad [centre - size/2 zoom, centre + size/2 zoom), nearest texel
+ * (GL_NEAREST, Graphics.h:90-91), alpha 1 inside [min, max] and 0 elsewhere, GL_FRAMEBUFFER_SRGB
+ * encode (byte = round(255 srgb(clamp(c, 0, 1))), exact; rmr_srgb_thresholds) and the
+ * SRC_ALPHA / ONE_MINUS_SRC_ALPHA blend: pixels drawn with alpha 1 are replaced, every other pixel
+ * keeps the caller's content (the GUI behind the image). rgba8 is a host buffer (in/out). */
+int rmr_display(rmr_ctx* ctx, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
+                float max_y, int screen_w, int screen_h, uint8_t* rgba8);
+/* The same into a device buffer (e.g. a torch uint8 tensor or an interop surface), on the context's
+ * stream, without host copies or a sync. */
+int rmr_display_device(rmr_ctx* ctx, float centre_x, float centre_y, float zoom, float min_x, float min_y,
+                       float max_x, float max_y, int screen_w, int screen_h, void* rgba8_dev);
+/* The 256 sRGB decision points rmr_display uses: out[k] = the smallest float c with byte(c) >= k. */
+int rmr_srgb_thresholds(float out[256]);
 /* Per-scene kernel specialisation (the reference recompiles its shader per scene, Graphics::Reload):
  * the scene's map() is generated as HIP source with the primitives as literals and compiled by
  * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under

@@ -1,0 +1,72 @@
+"""oracle/display.py — TEST INFRASTRUCTURE: numpy restatement of Graphics::Display (Graphics.cpp:356-390,
+createFQ 227-258, FullQuad.vs / FullQuad.fs) as rmr_display defines it headless; the checker of
+raymarchrenderer_amd's k_display (csrc/rmr_display.hip). Import only from tests/.
+
+Per screen pixel (row 0 = top), float32 arithmetic in the kernel's order:
+  h = (size / 2) * zoom; quad [c - h, c + h); fragment centre pos = pixel + 0.5 (rasterized if inside)
+  uv = (pos - (c - h)) / ((c + h) - (c - h)); texel = clamp(floor(uv * size))       (GL_NEAREST)
+  alpha 1 inside [min, max] (FullQuad.fs), else 0: alpha-1 pixels get sRGB8(texel.rgb), 255; every
+  other pixel keeps the background (SRC_ALPHA / ONE_MINUS_SRC_ALPHA blend)
+  sRGB8(c) = round(255 srgb(clamp(c, 0, 1))) exactly (GL_FRAMEBUFFER_SRGB), NaN -> 0
+"""
+import math
+
+import numpy as np
+
+F = np.float32
+
+
+def srgb_thresholds():
+    """thr[k] = the smallest float32 c with round(255 srgb(c)) >= k (k >= 1), thr[0] = 0: the bound
+    linear((k - 1/2) / 255) in double, rounded up to float32."""
+    thr = np.zeros(256, np.float32)
+    for k in range(1, 256):
+        y = (k - 0.5) / 255.0
+        lin = y / 12.92 if y <= 0.04045 else math.pow((y + 0.055) / 1.055, 2.4)
+        f = np.float32(lin)
+        if float(f) < lin:
+            f = np.nextafter(f, np.float32(2.0))
+        thr[k] = f
+    return thr
+
+
+def srgb8(c, thr=None):
+    thr = srgb_thresholds() if thr is None else thr
+    c = np.asarray(c, np.float32)
+    v = np.searchsorted(thr, np.where(np.isnan(c), F(0), c), side="right") - 1
+    v = np.where((c > 0) & ~np.isnan(c), v, 0)
+    return np.clip(v, 0, 255).astype(np.uint8)
+
+
+def srgb8_direct(c):
+    """The defining formula in float64 (for checking the thresholds; no exact-halfway inputs)."""
+    c = np.clip(np.nan_to_num(np.asarray(c, np.float64), nan=0.0), 0.0, 1.0)
+    s = np.where(c < 0.0031308, 12.92 * c, 1.055 * np.power(c, 1.0 / 2.4) - 0.055)
+    return np.floor(255.0 * s + 0.5).astype(np.uint8)
+
+
+def display(accum, centre, zoom, vmin, vmax, screen):
+    """accum (H, W, 4) float32 (row 0 = top); screen (h, w, 4) uint8 background; returns a new screen."""
+    H, W = accum.shape[:2]
+    sh, sw = screen.shape[:2]
+    out = screen.copy()
+    zoom = F(zoom)
+    hw = (F(W) / F(2)) * zoom
+    hh = (F(H) / F(2)) * zoom
+    cx, cy = F(centre[0]), F(centre[1])
+    x0, x1, y0, y1 = cx - hw, cx + hw, cy - hh, cy + hh
+    px = np.arange(sw, dtype=np.float32) + F(0.5)
+    py = np.arange(sh, dtype=np.float32) + F(0.5)
+    inx = (px >= x0) & (px < x1) & (px >= F(vmin[0])) & (px <= F(vmax[0]))
+    iny = (py >= y0) & (py < y1) & (py >= F(vmin[1])) & (py <= F(vmax[1]))
+    u = (px - x0) / (x1 - x0)
+    v = (py - y0) / (y1 - y0)
+    i = np.clip(np.floor(u * F(W)), 0, W - 1).astype(np.int64)
+    j = np.clip(np.floor(v * F(H)), 0, H - 1).astype(np.int64)
+    thr = srgb_thresholds()
+    m = iny[:, None] & inx[None, :]
+    tex = accum[j[:, None], i[None, :], :3]
+    rgb = srgb8(tex, thr)
+    out[..., :3] = np.where(m[..., None], rgb, out[..., :3])
+    out[..., 3] = np.where(m, np.uint8(255), out[..., 3])
+    return out

@@ -21,7 +21,8 @@ EXPORTS = [
     "rmr_accum_device_ptr", "rmr_bind_accum", "rmr_save_bmp", "rmr_encode_bmp",
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats", "rmr_get_section_cycles", "rmr_get_counters", "rmr_set_culling",
     "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_jit_compile_scene", "rmr_set_env_map",
-    "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free",
+    "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free", "rmr_display", "rmr_display_device",
+    "rmr_srgb_thresholds",
 ]
 
 
@@ -90,6 +91,9 @@ def lib():
         "rmr_scene_compile": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "rmr_scene_view": (C.c_int, [vp, C.POINTER(abi.Scene)]),
         "rmr_scene_free": (None, [vp]),
+        "rmr_display": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
+        "rmr_display_device": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
+        "rmr_srgb_thresholds": (C.c_int, [fp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

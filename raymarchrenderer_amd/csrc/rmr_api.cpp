@@ -25,6 +25,9 @@
 namespace rmr {
 hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool persistent, int grid, hipStream_t s);
 hipError_t launch_fold(const KParams& P, hipStream_t s);
+hipError_t launch_display(const float4* accum, int img_w, int img_h, float cx, float cy, float zoom, float min_x,
+                          float min_y, float max_x, float max_y, int scr_w, int scr_h, uint32_t* rgba8,
+                          const float* thr, hipStream_t s);
 int trace_occupancy(int variant, int np, bool prog, int* blocks_per_cu);
 }  // namespace rmr
 
@@ -64,6 +67,9 @@ struct rmr_ctx {
     float* d_esc = nullptr;
     double esc_infl_dev = -1.0;
     float4* d_env = nullptr;              // envTex (rmr_set_env_map)
+    float* d_srgb_thr = nullptr;          // rmr_display: sRGB decision points (256 floats)
+    uint32_t* d_screen = nullptr;         // rmr_display: staging of a host screen image
+    size_t screen_cap = 0;
     int env_w = 0, env_h = 0;
     int n_bvh = 0;
     float bvh_margin = 1e-4f;
@@ -761,7 +767,7 @@ void rmr_destroy(rmr_ctx* c) {
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
     void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_esc, c->d_env, c->d_samp,
-                    c->d_tiles, c->d_times, c->d_queue, c->d_counters};
+                    c->d_tiles, c->d_times, c->d_queue, c->d_counters, c->d_srgb_thr, c->d_screen};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
@@ -1064,6 +1070,69 @@ int rmr_set_kernel(rmr_ctx* c, int kernel) {
     if (!c || kernel < 0 || kernel > 1) return RMR_E_INVALID;
     c->kernel_mode = kernel;
     return RMR_OK;
+}
+
+// sRGB decision points of Graphics::Display's GL_FRAMEBUFFER_SRGB write: byte(c) = round(255 srgb(c))
+// for c in [0, 1] (srgb: 12.92 c below 0.0031308, else 1.055 c^(1/2.4) - 0.055), so byte(c) >= k
+// <=> srgb(c) >= (k - 1/2) / 255 <=> c >= linear((k - 1/2) / 255); out[k] is that bound rounded up to
+// a float (for a float c the comparison is then exact), out[0] = 0.
+int rmr_srgb_thresholds(float out[256]) {
+    if (!out) return RMR_E_INVALID;
+    out[0] = 0.0f;
+    for (int k = 1; k < 256; k++) {
+        const double y = (k - 0.5) / 255.0;
+        const double lin = (y <= 0.04045) ? y / 12.92 : std::pow((y + 0.055) / 1.055, 2.4);
+        float f = (float)lin;
+        if ((double)f < lin) f = std::nextafter(f, 2.0f);
+        out[k] = f;
+    }
+    return RMR_OK;
+}
+
+namespace {
+int display_common(rmr_ctx* c, float cx, float cy, float zoom, float min_x, float min_y, float max_x, float max_y,
+                   int sw, int sh, uint32_t* dev) {
+    if (!c->d_srgb_thr) {
+        float t[256];
+        rmr_srgb_thresholds(t);
+        int r = dev_upload(c, &c->d_srgb_thr, t, 256);
+        if (r) return r;
+    }
+    HIPCHK(c, rmr::launch_display(c->d_accum, c->W, c->H, cx, cy, zoom, min_x, min_y, max_x, max_y, sw, sh, dev,
+                                  c->d_srgb_thr, c->stream));
+    return RMR_OK;
+}
+}  // namespace
+
+int rmr_display(rmr_ctx* c, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
+                float max_y, int screen_w, int screen_h, uint8_t* rgba8) {
+    if (!c || !rgba8 || screen_w <= 0 || screen_h <= 0 || screen_w > 32768 || screen_h > 32768)
+        return fail(c, RMR_E_INVALID, "rmr_display: bad screen image");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t n = (size_t)screen_w * screen_h;
+    if (n > c->screen_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->d_screen) (void)hipFree(c->d_screen);
+        c->d_screen = nullptr;
+        c->screen_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_screen, n * sizeof(uint32_t)));
+        c->screen_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_screen, rgba8, n * 4, hipMemcpyHostToDevice, c->stream));
+    int r = display_common(c, centre_x, centre_y, zoom, min_x, min_y, max_x, max_y, screen_w, screen_h, c->d_screen);
+    if (r) return r;
+    HIPCHK(c, hipMemcpyAsync(rgba8, c->d_screen, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RMR_OK;
+}
+
+int rmr_display_device(rmr_ctx* c, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
+                       float max_y, int screen_w, int screen_h, void* rgba8_dev) {
+    if (!c || !rgba8_dev || screen_w <= 0 || screen_h <= 0 || screen_w > 32768 || screen_h > 32768)
+        return fail(c, RMR_E_INVALID, "rmr_display_device: bad screen image");
+    HIPCHK(c, hipSetDevice(c->device));
+    return display_common(c, centre_x, centre_y, zoom, min_x, min_y, max_x, max_y, screen_w, screen_h,
+                          (uint32_t*)rgba8_dev);
 }
 
 int rmr_set_env_map(rmr_ctx* c, const uint8_t* rgba8, int w, int h) {

@@ -230,6 +230,26 @@ class Renderer:
         _check(self._ctx, lib().rmr_load_accum(self._ctx, path.encode(), C.byref(n)))
         return n.value
 
+    def display(self, centre, zoom, vmin, vmax, screen=None, screen_size=None):
+        """Graphics::Display(centre, zoom, min, max) headless (rmr_display): the accumulator drawn into
+        an RGBA8 screen image (h, w, 4) uint8, row 0 = top. `screen` is the image behind it (kept
+        where the quad draws alpha 0); without it a zeroed image of `screen_size` (w, h)."""
+        if screen is None:
+            w, h = screen_size
+            screen = np.zeros((int(h), int(w), 4), np.uint8)
+        screen = np.ascontiguousarray(screen, np.uint8)
+        h, w = screen.shape[:2]
+        _check(self._ctx, lib().rmr_display(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
+                                            float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
+                                            w, h, screen.ctypes.data))
+        return screen
+
+    def display_device(self, centre, zoom, vmin, vmax, dev_ptr, screen_w, screen_h):
+        """rmr_display_device: the same into a device RGBA8 buffer on the renderer's stream."""
+        _check(self._ctx, lib().rmr_display_device(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
+                                                   float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
+                                                   int(screen_w), int(screen_h), C.c_void_p(dev_ptr)))
+
     def stats(self):
         s = abi.Stats()
         _check(self._ctx, lib().rmr_get_stats(self._ctx, C.byref(s)))
@@ -341,6 +361,12 @@ class Graphics:
         Graphics._r.save_bmp(path)
 
     @staticmethod
+    def Display(centre, zoom, vmin, vmax, screen=None):
+        """Graphics::Display (Graphics.cpp:356-390) into a screen image of Screen.getScreenSize()."""
+        size = tuple(int(v) for v in Screen.getScreenSize())
+        return Graphics._r.display(centre, zoom, vmin, vmax, screen=screen, screen_size=size)
+
+    @staticmethod
     def addMaterial(material):
         Graphics._materials.append(material)
 
@@ -426,3 +452,12 @@ def save_name(now=None):
     """Program.cpp:71-84 file name: output\\%Y-%m-%d_%H-%M-%S.bmp."""
     t = _time.localtime(now)
     return _time.strftime("%Y-%m-%d_%H-%M-%S", t) + ".bmp"
+
+
+def srgb_thresholds():
+    """rmr_srgb_thresholds: the 256 linear-space decision points of the display's sRGB encode."""
+    out = np.zeros(256, np.float32)
+    rc = lib().rmr_srgb_thresholds(_fp(out))
+    if rc != abi.RMR_OK:
+        raise RMRError(rc, "rmr_srgb_thresholds")
+    return out

@@ -36,6 +36,9 @@ CASES = {
     "rm2_simple_env": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}, 40.0),
     # round 2: RM1's object node set (op_* / domain_repeat / math / misc)
     "rm1_csg_nodes_b4": (os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}, 40.0),
+    # C3's Mandelbulb node in the reference path (oracle/glsl_ref/shader_build.py X1; the driver's own
+    # transcendentals, so the distance estimate agrees to ~3e-5 and the images by PSNR)
+    "rm1_mandelbulb_b2": (os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}, 40.0),
 }
 
 
