@@ -44,6 +44,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("librmr.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                            "(expected at %s)" % LIB_PATH)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, and once librmr has brought
+    # in /opt/rocm's, torch can no longer initialise the GPU ("No HIP GPUs are available", measured on
+    # the MI355X box). Loading torch first makes librmr bind to the runtime already in the process, so
+    # torch tensors and rmr contexts can share one device (FrameRenderer, rmr_bind_accum).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, fp, ip = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)
     dp = C.POINTER(C.c_double)
