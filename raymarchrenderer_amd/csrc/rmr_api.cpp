@@ -96,6 +96,7 @@ struct rmr_ctx {
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
     int full_threshold = 40 | (2 << 8);   // nearest-primitive cache: 40 lanes per full map() batch, R = 2 (csg256)
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
+    int sched = RMR_SCHED_MEGA;    // rmr_set_schedule
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels)
@@ -322,7 +323,8 @@ int ensure_jit(rmr_ctx* c) {
             if (std::memcmp(&prims[j], &c->jit_base[j], sizeof(rmr_prim)) != 0) c->jit_live[j] = 1;
     }
     c->jit_struct_src = struct_src;
-    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live);
+    const bool split = c->sched == RMR_SCHED_SPLIT && rmr::jit_split_applies(c->scene, c->has_prog, c->cull);
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, split);
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {
@@ -349,12 +351,17 @@ int ensure_jit(rmr_ctx* c) {
         c->jit_failed = true;
         return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
     }
+    k.block = split ? rmr::kSplitBlock : 256;
     int b = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, 256, 0) != hipSuccess || b <= 0) b = 4;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = split ? 2 : 4;
     k.blocks_per_cu = b;
     // RM1 inline sphere/box maps: 20 (C2 +2%); general maps without material programs, whose
     // map() dwarfs the shading (the Mandelbulb): 8 (C3 +2-3%); otherwise 16
-    if (src.find("rmr::trace_waves<1, false, false>") != std::string::npos && src.find("TableMap<") == std::string::npos)
+    // split kernels: lanes a marching wave collects before handing finished marches over (and idle
+    // lanes before it refills)
+    if (split)
+        k.shade_t = 6;
+    else if (src.find("rmr::trace_waves<1, false, false>") != std::string::npos && src.find("TableMap<") == std::string::npos)
         k.shade_t = 20;
     else if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
         k.shade_t = 8;
@@ -675,7 +682,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
         if (use_jit) {
             void* args[] = {&P};
-            HIPCHK(c, hipModuleLaunchKernel(c->jit.fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+            HIPCHK(c, hipModuleLaunchKernel(c->jit.fn, (unsigned)grid, 1, 1, (unsigned)c->jit.block, 1, 1, 0, c->stream, args,
+                                            nullptr));
             c->stats.jit_launches++;
         } else {
             HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
@@ -749,6 +757,7 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
     if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
     if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
+    if (const char* e = std::getenv("RMR_SPLIT")) c->sched = std::atoi(e) ? RMR_SCHED_SPLIT : RMR_SCHED_MEGA;
     if (const char* e = std::getenv("RMR_FULL_T"))
         c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RMR_FULL_R"))
@@ -1026,8 +1035,9 @@ int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
     if (!c || !out) return RMR_E_INVALID;
     int r = rmr_sync(c);
     if (r) return r;
-    unsigned long long cnt[4];
+    unsigned long long cnt[16];
     HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+    if (cnt[14]) return fail(c, RMR_E_HIP, "split trace kernel: a workgroup's wait timed out (" + std::to_string(cnt[14]) + ")");
     c->stats.map_evals = cnt[0];
     c->stats.map_iters = cnt[1];
     c->stats.shade_batches = cnt[2];
@@ -1169,6 +1179,13 @@ int rmr_set_culling(rmr_ctx* c, int flags) {
     return RMR_OK;
 }
 
+int rmr_set_schedule(rmr_ctx* c, int schedule) {
+    if (!c || (schedule != RMR_SCHED_MEGA && schedule != RMR_SCHED_SPLIT)) return RMR_E_INVALID;
+    if (schedule != c->sched) c->jit_ready = false;   // the specialised kernel depends on it
+    c->sched = schedule;
+    return RMR_OK;
+}
+
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen) {
     std::string lg;
     try {
@@ -1184,7 +1201,7 @@ int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, 
         }
         std::vector<char> code;
         std::string key;
-        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog), code, key, lg);
+        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog, true, 7, nullptr, false), code, key, lg);
         if (log && loglen) std::snprintf(log, loglen, "%s", ok ? key.c_str() : lg.c_str());
         return ok ? RMR_OK : RMR_E_HIP;
     } catch (const std::exception& e) {

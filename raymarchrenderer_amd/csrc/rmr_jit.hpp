@@ -23,7 +23,12 @@ struct JitKernel {
     hipFunction_t fn = nullptr;
     int blocks_per_cu = 0;
     int shade_t = 16;           // default shading batch size for this kernel (rmr_api.cpp)
+    int block = 256;            // workgroup size (march / shade split kernels: 64 x RMR_SPLIT_WAVES)
 };
+// Workgroup size of the split kernels (rmr_trace.h trace_split: RMR_SPLIT_WAVES waves)
+constexpr int kSplitBlock = 512;
+// The split schedule applies to this specialisation (HO kernel without the nearest-primitive cache)
+bool jit_split_applies(const CompiledScene& s, bool prog, int cull);
 
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the
 // primitives' numbers are literals (fastest: +6-12% over loading them); otherwise only the scene's
@@ -32,8 +37,9 @@ struct JitKernel {
 // cull: RMR_CULL_* bits of the context (rmr.h): approximate-then-exact map, nearest-primitive cache.
 // live (with bake): primitives j with live[j] != 0 are loaded even so (an animation's moving
 // primitives; the rest stay literals).
+// split: the march / shade split schedule where it applies (jit_split_applies).
 std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
-                       const std::vector<char>* live = nullptr);
+                       const std::vector<char>* live = nullptr, bool split = true);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);

@@ -1747,6 +1747,501 @@ RMR_D void trace_main(const KParams& P) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// March / shade split (persistent HO kernels without the nearest-primitive cache: RM1 with the fast
+// materials, RM3; the hipRTC kernels, rmr_jit.cpp). In trace_main every wave both marches and
+// shades: shading batches run with the ~20 lanes that wait (a quarter to a third of the wave) while
+// those lanes sit out map() iterations. Here a workgroup of RMR_SPLIT_WAVES waves has one shading
+// wave and RMR_SPLIT_WAVES - 1 marching waves that exchange paths through LDS rings:
+//  * a marching wave only runs map() iterations (march steps and getNormal probes). A lane whose
+//    march ends (HIT: normal done, or MISS) is pushed to the wave's hit ring and refilled from the
+//    wave's ray ring;
+//  * the shading wave pops hits into its free lanes from every hit ring and shades them full-width,
+//    starts fresh units (primary rays, begin_trace) in lanes left free, and pushes every new ray
+//    (bounce or primary) to the ray rings. It runs at raised priority: a marching wave waits for
+//    it, never the other way round.
+// Each path runs exactly the trace_main arithmetic (the same functions on the same Lane state), so
+// every sample is bit-identical; only which lane and which wave executes a step changes.
+// Rings are single-producer single-consumer (head/tail in LDS, workgroup-scope release/acquire).
+// No deadlock: the shading wave starts a path only while the paths in flight stay below
+// 64 x waves + 2 x rings x RMR_SPLIT_RING - 1, so the hit rings, the ray rings, the marching lanes
+// and the shading lanes can never all be full at once. Every wait is also bounded in time
+// (RMR_SPLIT_WAIT shader clocks without progress): the workgroup then exits and counts the event in
+// P.counters[14], which the host reports as an error.
+// ------------------------------------------------------------------------------------------
+#ifndef RMR_SPLIT_WAVES
+#define RMR_SPLIT_WAVES 8   // waves per workgroup: 1 shading + RMR_SPLIT_WAVES - 1 marching
+#endif
+#ifndef RMR_SPLIT_RING
+#define RMR_SPLIT_RING 32   // entries of each marching wave's ray ring and hit ring (power of two)
+#endif
+#ifndef RMR_SPLIT_WAIT
+#define RMR_SPLIT_WAIT (1ull << 31)
+#endif
+#ifndef RMR_SPLIT_PRIO
+#define RMR_SPLIT_PRIO 2
+#endif
+#ifndef RMR_SPLIT_SLEEP
+#define RMR_SPLIT_SLEEP 2   // s_sleep units (64 clocks) of the shading wave's idle poll
+#endif
+constexpr int kSplitMarch = RMR_SPLIT_WAVES - 1;
+constexpr uint32_t kRingMask = RMR_SPLIT_RING - 1;
+static_assert((RMR_SPLIT_RING & (RMR_SPLIT_RING - 1)) == 0, "ring size must be a power of two");
+struct RayRec { float4 a, b, c, d; };      // o.xyz texit | d.xyz flags | rc gxt gyt unit | color / power wl, bounces
+struct HitRec { float4 a, b, c, d, e; };   // o.xyz mid | d.xyz flags | rc gxt gyt unit | color.., bounces | nrm.xyz t
+struct SplitLds {
+    RayRec ray[kSplitMarch][RMR_SPLIT_RING];
+    HitRec hit[kSplitMarch][RMR_SPLIT_RING];
+    uint32_t ray_tail[kSplitMarch], ray_head[kSplitMarch], hit_tail[kSplitMarch], hit_head[kSplitMarch];
+    uint32_t done;     // 1: every path of the workgroup finished; 2: a wait timed out
+    uint32_t events;   // hand-overs and refills of the marching waves (the shading wave's idle poll)
+};
+RMR_D uint32_t lds_acquire(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+RMR_D void lds_release(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// flags word: phase (bits 0-3), chan + 1 (4-7), inside (8)
+RMR_D float pack_flags(const Lane& L) {
+    return __int_as_float((L.phase & 15) | ((L.chan + 1) << 4) | ((int)L.inside << 8));
+}
+RMR_D void unpack_flags(Lane& L, float f) {
+    const int v = __float_as_int(f);
+    L.phase = v & 15;
+    L.chan = ((v >> 4) & 15) - 1;
+    L.inside = ((v >> 8) & 1) != 0;
+}
+template <int VAR>
+RMR_D float4 pack_payload(const Lane& L) {   // throughput (RM1 color, RM3 power + hero wavelength), bounces
+    if constexpr (VAR == RMR_VARIANT_RM3) return make_float4(L.power, __uint_as_float(L.wl), 0.0f, __int_as_float(L.bounces));
+    else return make_float4(L.color.x, L.color.y, L.color.z, __int_as_float(L.bounces));
+}
+template <int VAR>
+RMR_D void unpack_payload(Lane& L, float4 v) {
+    if constexpr (VAR == RMR_VARIANT_RM3) {
+        L.power = v.x;
+        L.wl = __float_as_uint(v.y);
+    } else {
+        L.color = v3(v.x, v.y, v.z);
+    }
+    L.bounces = __float_as_int(v.w);
+}
+template <int VAR>
+RMR_D void put_ray(RayRec& r, const Lane& L) {
+    r.a = make_float4(L.o.x, L.o.y, L.o.z, L.texit);
+    r.b = make_float4(L.d.x, L.d.y, L.d.z, pack_flags(L));
+    r.c = make_float4(L.rc, L.gxt, L.gyt, __uint_as_float(L.unit));
+    r.d = pack_payload<VAR>(L);
+}
+template <int VAR>
+RMR_D void get_ray(Lane& L, const RayRec& r) {   // a ray as start_march left it: t = 0, ctr = 0
+    const float4 a = r.a, b = r.b, c = r.c, d = r.d;
+    L.o = v3(a.x, a.y, a.z);
+    L.texit = a.w;
+    L.d = v3(b.x, b.y, b.z);
+    unpack_flags(L, b.w);
+    L.rc = c.x; L.gxt = c.y; L.gyt = c.z; L.unit = __float_as_uint(c.w);
+    unpack_payload<VAR>(L, d);
+    L.t = 0.0f;
+    L.ctr = 0;
+}
+template <int VAR>
+RMR_D void put_hit(HitRec& h, const Lane& L) {
+    h.a = make_float4(L.o.x, L.o.y, L.o.z, L.mid);
+    h.b = make_float4(L.d.x, L.d.y, L.d.z, pack_flags(L));
+    h.c = make_float4(L.rc, L.gxt, L.gyt, __uint_as_float(L.unit));
+    h.d = pack_payload<VAR>(L);
+    h.e = make_float4(L.nrm.x, L.nrm.y, L.nrm.z, L.t);
+}
+template <int VAR>
+RMR_D void get_hit(Lane& L, const HitRec& h) {
+    const float4 a = h.a, b = h.b, c = h.c, d = h.d, e = h.e;
+    L.o = v3(a.x, a.y, a.z);
+    L.mid = a.w;
+    L.d = v3(b.x, b.y, b.z);
+    unpack_flags(L, b.w);
+    L.rc = c.x; L.gxt = c.y; L.gyt = c.z; L.unit = __float_as_uint(c.w);
+    unpack_payload<VAR>(L, d);
+    L.nrm = v3(e.x, e.y, e.z);
+    L.t = e.w;
+    L.ctr = 0;
+}
+RMR_D uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// A pair of ring index arrays (tails, heads) of a workgroup, read in one LDS round trip (relaxed
+// loads, then one acquire fence), as wave-uniform (scalar) values.
+RMR_D void ring_idx(const uint32_t* tails, const uint32_t* heads, uint32_t (&t)[kSplitMarch], uint32_t (&h)[kSplitMarch]) {
+#pragma unroll
+    for (int w = 0; w < kSplitMarch; w++) {
+        t[w] = __hip_atomic_load(&tails[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        h[w] = __hip_atomic_load(&heads[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int w = 0; w < kSplitMarch; w++) {
+        t[w] = __builtin_amdgcn_readfirstlane(t[w]);
+        h[w] = __builtin_amdgcn_readfirstlane(h[w]);
+    }
+}
+// Spread `want` items over the rings, ring rr first: ring w gets take[w] <= avail[w], in rotated
+// order; lane `rank` (< the total taken) is told its ring `mw` and its offset `off` in that ring's
+// share. Static indices only (no register-array indexing by a variable).
+RMR_D uint32_t ring_spread(const uint32_t (&avail)[kSplitMarch], uint32_t want, uint32_t rr, uint32_t rank,
+                           uint32_t (&take)[kSplitMarch], int& mw, uint32_t& off) {
+    uint32_t before_rr = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kSplitMarch; w++) {
+        before_rr += (uint32_t)w < rr ? avail[w] : 0u;
+        total += avail[w];
+    }
+    uint32_t pre = 0;   // sum of avail over rings w' < w
+    mw = -1;
+    off = 0;
+    uint32_t got = 0;
+#pragma unroll
+    for (int w = 0; w < kSplitMarch; w++) {
+        const uint32_t start = (uint32_t)w >= rr ? pre - before_rr : pre + (total - before_rr);
+        const uint32_t room = want > start ? want - start : 0u;
+        take[w] = avail[w] < room ? avail[w] : room;
+        if (rank >= start && rank < start + take[w]) { mw = w; off = rank - start; }
+        got += take[w];
+        pre += avail[w];
+    }
+    return got;
+}
+
+#ifdef RMR_SPLIT_STATS   // diagnostics (RMR_JIT_OPTS=-DRMR_SPLIT_STATS): cycle split of the two roles
+#define RMR_SSTAT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define RMR_SSTAT(v)
+#endif
+#ifndef RMR_SPLIT_QLOW
+#define RMR_SPLIT_QLOW (kSplitMarch * RMR_SPLIT_RING / 2)   // queued rays below which partial batches run
+#endif
+#ifndef RMR_SPLIT_INFLIGHT   // paths a workgroup keeps in flight (marching lanes + a batch + queued rays)
+#define RMR_SPLIT_INFLIGHT (64 * RMR_SPLIT_WAVES + kSplitMarch * RMR_SPLIT_RING / 2)
+#endif
+// Ray-ring shares that level the rings' occupancies (water filling): ring w may take
+// max(0, min(lv, RING) - occ[w]) with the smallest level lv that places `want` rays (or all free slots).
+RMR_D void ring_level(const uint32_t (&occ)[kSplitMarch], uint32_t want, uint32_t (&avail)[kSplitMarch]) {
+    uint32_t lo = 0, hi = RMR_SPLIT_RING;
+    while (lo < hi) {
+        const uint32_t lv = (lo + hi) >> 1;
+        uint32_t f = 0;
+#pragma unroll
+        for (int w = 0; w < kSplitMarch; w++) f += lv > occ[w] ? lv - occ[w] : 0u;
+        if (f >= want) hi = lv;
+        else lo = lv + 1;
+    }
+#pragma unroll
+    for (int w = 0; w < kSplitMarch; w++) avail[w] = lo > occ[w] ? lo - occ[w] : 0u;
+}
+
+// the shading wave of a workgroup
+template <int VAR, class MATS>
+RMR_D void split_shade(const KParams& P, SplitLds& S) {
+    constexpr bool HO = true;
+    __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
+    Lane L;
+    L.phase = PH_IDLE;
+    L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
+    const uint64_t n_units = P.n_units;
+    const uint32_t cap = 64u * RMR_SPLIT_WAVES + 2u * kSplitMarch * RMR_SPLIT_RING - 1u;
+    const uint32_t target = (uint32_t)RMR_SPLIT_INFLIGHT < cap ? (uint32_t)RMR_SPLIT_INFLIGHT : cap;
+    uint32_t in_flight = 0, rr = 0;
+    bool exhausted = false;
+    uint64_t shades = 0, shaded = 0;
+    uint64_t t_prog = __builtin_amdgcn_s_memtime();   // start of the current wait (no progress)
+    bool waiting = false;
+#ifdef RMR_SPLIT_STATS
+    uint64_t cyc_hit = 0, cyc_fresh = 0, n_hitb = 0, n_freshb = 0;
+    const uint64_t c_begin = t_prog;
+#endif
+    uint32_t last_ev = 0xffffffffu;   // S.events at the last iteration without progress
+    for (;;) {
+        bool progress = false, hb = false, fb = false;
+        const uint32_t ev = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&S.events, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (ev == last_ev) {   // nothing to do then, and no marching wave has acted since
+            if (lds_acquire(&S.done) == 2u) break;
+            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
+                if (__lane_id() == 0) {
+                    lds_release(&S.done, 2u);
+                    atomicAdd(P.counters + 14, 1ull);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_sleep(RMR_SPLIT_SLEEP);
+            __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
+            continue;
+        }
+        uint32_t ht[kSplitMarch], hh[kSplitMarch];
+        uint32_t H = 0, Q = 0;
+        {
+            uint32_t rt[kSplitMarch], rh[kSplitMarch];
+            ring_idx(S.ray_tail, S.ray_head, rt, rh);
+            ring_idx(S.hit_tail, S.hit_head, ht, hh);
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++) { H += ht[w] - hh[w]; Q += rt[w] - rh[w]; }
+        }
+        const uint64_t idle = __ballot(L.phase == PH_IDLE);
+        const uint32_t nidle = (uint32_t)__popcll(idle), rank = lane_rank(idle);
+        const uint32_t pend = 64u - nidle;   // lanes holding a ray not yet pushed
+        const bool starving = Q + pend < (uint32_t)RMR_SPLIT_QLOW;
+        RMR_SSTAT(c0);
+        if (nidle && H && (H >= nidle || starving || exhausted)) {
+            // 1. a shading batch: hits into the free lanes, from every hit ring (ring rr first)
+            uint32_t avail[kSplitMarch], take[kSplitMarch];
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++) avail[w] = ht[w] - hh[w];
+            int mw;
+            uint32_t off;
+            ring_spread(avail, nidle, rr, rank, take, mw, off);
+            uint32_t slot = 0;
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++) slot = mw == w ? hh[w] + off : slot;
+            if (L.phase == PH_IDLE && mw >= 0) get_hit<VAR>(L, S.hit[mw][slot & kRingMask]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++)
+                if (take[w]) __hip_atomic_store(&S.hit_head[w], hh[w] + take[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            rr = rr + 1 == (uint32_t)kSplitMarch ? 0 : rr + 1;
+            progress = hb = true;
+        } else if (nidle && !exhausted && in_flight < target) {
+            // 2. fresh units (primary rays) into the free lanes, up to the in-flight target
+            uint32_t take = nidle < target - in_flight ? nidle : target - in_flight;
+            if (take) {
+                unsigned long long b = 0;
+                if (__lane_id() == 0) b = atomicAdd(P.queue, (unsigned long long)take);
+                b = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                    (unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)b);
+                if (L.phase == PH_IDLE && rank < take && b + rank < n_units)
+                    begin_trace<VAR, HO>(P, L, (uint32_t)(b + rank), true);
+                exhausted = b + take >= n_units;
+                in_flight += (uint32_t)__popcll(__ballot(L.phase != PH_IDLE)) - pend;
+                progress = fb = true;
+            }
+        }
+        RMR_SSTAT(c1);
+        // 3. shade until every lane is free or holds a new ray (a ray may miss at once: escape bound;
+        // a path can also be done straight from begin_trace: zero bounces)
+        for (;;) {
+            const uint64_t fin = __ballot(L.phase == PH_DONE);
+            in_flight -= (uint32_t)__popcll(fin);
+            if (L.phase == PH_DONE) L.phase = PH_IDLE;
+            const uint64_t sm = __ballot(is_shade(L.phase));
+            if (!sm) break;
+            shades++;
+            shaded += (uint64_t)__popcll(sm);
+            if (is_shade(L.phase)) shade<VAR, false, MATS>(P, L);
+            const bool restart = (L.phase == PH_RESTART);
+            if (__ballot(restart)) {
+                if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
+            }
+        }
+        RMR_SSTAT(c2);
+#ifdef RMR_SPLIT_STATS
+        (void)c1;
+        if (hb) { n_hitb++; cyc_hit += c2 - c0; }
+        if (fb) { n_freshb++; cyc_fresh += c2 - c0; }
+#else
+        (void)hb; (void)fb;
+#endif
+        // 4. new rays to the ray rings (ring rr first; consecutive rays of a batch stay together)
+        const uint64_t pm = __ballot(L.phase == PH_MARCH);
+        if (pm) {
+            uint32_t rt[kSplitMarch], rh[kSplitMarch], avail[kSplitMarch], take[kSplitMarch];
+            ring_idx(S.ray_tail, S.ray_head, rt, rh);
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++) avail[w] = rt[w] - rh[w];   // occupancy
+            ring_level(avail, (uint32_t)__popcll(pm), avail);
+            int mw;
+            uint32_t off;
+            const uint32_t got = ring_spread(avail, (uint32_t)__popcll(pm), rr, lane_rank(pm), take, mw, off);
+            uint32_t slot = 0;
+#pragma unroll
+            for (int w = 0; w < kSplitMarch; w++) slot = mw == w ? rt[w] + off : slot;
+            if (L.phase == PH_MARCH && mw >= 0) {
+                put_ray<VAR>(S.ray[mw][slot & kRingMask], L);
+                L.phase = PH_IDLE;
+            }
+            if (got) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+                for (int w = 0; w < kSplitMarch; w++)
+                    if (take[w]) __hip_atomic_store(&S.ray_tail[w], rt[w] + take[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                progress = true;
+            }
+        }
+        if (exhausted && in_flight == 0) {
+            if (__lane_id() == 0) lds_release(&S.done, 1u);
+            break;
+        }
+        if (progress) {
+            waiting = false;
+            last_ev = 0xffffffffu;
+        } else {
+            last_ev = ev;
+            if (!waiting) {
+                waiting = true;
+                t_prog = __builtin_amdgcn_s_memtime();
+            }
+            if (lds_acquire(&S.done) == 2u) break;
+            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
+                if (__lane_id() == 0) {
+                    lds_release(&S.done, 2u);
+                    atomicAdd(P.counters + 14, 1ull);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_setprio(0);   // polling: at the marching waves' priority
+            __builtin_amdgcn_s_sleep(RMR_SPLIT_SLEEP);
+            __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
+        }
+    }
+    if (__lane_id() == 0) {
+        atomicAdd(P.counters + 2, (unsigned long long)shades);
+        atomicAdd(P.counters + 8, (unsigned long long)shaded);
+#ifdef RMR_SPLIT_STATS
+        atomicAdd(P.counters + 4, (unsigned long long)n_hitb);
+        atomicAdd(P.counters + 5, (unsigned long long)n_freshb);
+        atomicAdd(P.counters + 6, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
+        atomicAdd(P.counters + 7, (unsigned long long)cyc_hit);
+        atomicAdd(P.counters + 9, (unsigned long long)cyc_fresh);
+#endif
+    }
+}
+
+// a marching wave of a workgroup (ring index w). One loop iteration = one map() step for every
+// active lane; the ray ring's tail is read (relaxed) at the top of the iteration and used after the
+// step, so its latency hides behind the map. Finished marches are handed over once T lanes wait (or
+// no lane is active); idle lanes are refilled once TR of them wait (or no lane is active).
+template <int VAR, class MAP>
+RMR_D void split_march(const KParams& P, SplitLds& S, int w) {
+    constexpr bool HO = true;
+    Lane L;
+    L.phase = PH_IDLE;
+    L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
+    uint32_t ray_head = 0, hit_tail = 0, hit_head = 0;   // hit_head: last value seen (the shading wave owns it)
+    uint64_t maps = 0, iters = 0;
+    const int T = P.shade_threshold, TR = P.refill_threshold;
+    uint64_t t_prog = __builtin_amdgcn_s_memtime();   // start of the current wait (no progress)
+    bool waiting = false;
+#ifdef RMR_SPLIT_STATS
+    uint64_t cyc_starved = 0, last_c0 = t_prog;
+    bool last_starved = false;
+    const uint64_t c_begin = t_prog;
+#endif
+    for (;;) {
+        bool progress = false;
+#ifdef RMR_SPLIT_STATS
+        RMR_SSTAT(c0);
+        if (last_starved) cyc_starved += c0 - last_c0;
+        last_c0 = c0;
+#endif
+        const uint32_t ray_tail = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&S.ray_tail[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        uint64_t am = __ballot(is_active(L.phase));
+#ifdef RMR_SPLIT_STATS
+        last_starved = am == 0;
+#endif
+        if (am) {   // one map() step
+            if (is_active(L.phase)) {
+                const V3 p = RMR_MARCH_POINT(L);
+                if constexpr (!MAP::kCounts)
+                    RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
+                const V2 m = MAP::eval(P, p);
+                if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                else march_update<HO>(P, L, m);
+            }
+            maps += (uint64_t)__popcll(am);
+            iters++;
+            am = __ballot(is_active(L.phase));
+            progress = true;
+        }
+        // hand finished marches to the shading wave
+        const uint64_t sm = __ballot(is_shade(L.phase));
+        if (sm && (__popcll(sm) >= T || am == 0)) {
+            const uint32_t nsm = (uint32_t)__popcll(sm);
+            if (RMR_SPLIT_RING - (hit_tail - hit_head) < nsm) hit_head = __builtin_amdgcn_readfirstlane(lds_acquire(&S.hit_head[w]));
+            const uint32_t freeh = RMR_SPLIT_RING - (hit_tail - hit_head);
+            const uint32_t n = freeh < nsm ? freeh : nsm;
+            if (n) {
+                const uint32_t rank = lane_rank(sm);
+                if (is_shade(L.phase) && rank < n) {
+                    put_hit<VAR>(S.hit[w][(hit_tail + rank) & kRingMask], L);
+                    L.phase = PH_IDLE;
+                }
+                hit_tail += n;
+                lds_release(&S.hit_tail[w], hit_tail);
+                if (__lane_id() == 0) __hip_atomic_fetch_add(&S.events, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                progress = true;
+            }
+        }
+        // refill idle lanes from the ray ring
+        const uint64_t idle = __ballot(L.phase == PH_IDLE);
+        if (idle && (__popcll(idle) >= TR || am == 0) && ray_tail != ray_head) {
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            const uint32_t n = ray_tail - ray_head < nidle ? ray_tail - ray_head : nidle;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const uint32_t rank = lane_rank(idle);
+            if (L.phase == PH_IDLE && rank < n) get_ray<VAR>(L, S.ray[w][(ray_head + rank) & kRingMask]);
+            ray_head += n;
+            lds_release(&S.ray_head[w], ray_head);
+            if (__lane_id() == 0) __hip_atomic_fetch_add(&S.events, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            progress = true;
+        }
+        if (progress) {
+            waiting = false;
+        } else {
+            if (!waiting) {
+                waiting = true;
+                t_prog = __builtin_amdgcn_s_memtime();
+            }
+            const uint32_t dn = lds_acquire(&S.done);
+            if (dn == 2u || (dn == 1u && !__ballot(L.phase != PH_IDLE))) break;
+            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
+                if (__lane_id() == 0) {
+                    lds_release(&S.done, 2u);
+                    atomicAdd(P.counters + 14, 1ull);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (__lane_id() == 0) {
+        atomicAdd(P.counters + 0, (unsigned long long)maps);
+        atomicAdd(P.counters + 1, (unsigned long long)iters);
+#ifdef RMR_SPLIT_STATS
+        atomicAdd(P.counters + 10, (unsigned long long)cyc_starved);
+        atomicAdd(P.counters + 15, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
+#endif
+    }
+}
+
+// kernel body of a split workgroup (blockDim.x == 64 * RMR_SPLIT_WAVES). The shading role rotates
+// with the workgroup index, so the shading waves of a CU's workgroups spread over its SIMDs.
+template <int VAR, class MAP, class MATS = TableMats>
+RMR_D void trace_split(const KParams& P) {
+    static_assert(hit_in_origin<VAR, false>() && !MAP::kCache, "split kernels: HO kernels without the cache");
+    __shared__ SplitLds S;
+    if (threadIdx.x < (unsigned)kSplitMarch) {
+        S.ray_tail[threadIdx.x] = 0; S.ray_head[threadIdx.x] = 0;
+        S.hit_tail[threadIdx.x] = 0; S.hit_head[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) { S.done = 0; S.events = 0; }
+    __syncthreads();
+    const int wave = (int)(threadIdx.x >> 6);
+    const int shader = (int)(blockIdx.x % RMR_SPLIT_WAVES);
+    if (wave == shader) split_shade<VAR, MATS>(P, S);
+    else split_march<VAR, MAP>(P, S, wave < shader ? wave : wave - 1);
+}
+
 // Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
 RMR_D void fold_main(const KParams& P) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;

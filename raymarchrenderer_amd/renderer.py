@@ -170,6 +170,11 @@ class Renderer:
         """Exact work-skipping switches (abi.CULL_*; results are bit-identical either way)."""
         _check(self._ctx, lib().rmr_set_culling(self._ctx, int(flags)))
 
+    def set_schedule(self, schedule):
+        """Wave scheduling of the specialised kernels: abi.SCHED_MEGA (every wave marches and shades)
+        (default) or abi.SCHED_SPLIT (one shading wave per seven marching waves). Bit-identical."""
+        _check(self._ctx, lib().rmr_set_schedule(self._ctx, int(schedule)))
+
     def set_stream(self, hip_stream_handle):
         _check(self._ctx, lib().rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
 
@@ -257,6 +262,12 @@ class Renderer:
 
     def reset_stats(self):
         _check(self._ctx, lib().rmr_reset_stats(self._ctx))
+
+    def counters(self):
+        """The kernels' 16 raw device counters (rmr_get_counters; rmr_trace.h documents the slots)."""
+        raw = (C.c_uint64 * 16)()
+        _check(self._ctx, lib().rmr_get_counters(self._ctx, raw))
+        return [int(v) for v in raw]
 
 
 def jit_compile_scene(scene, variant):
