@@ -168,6 +168,27 @@ RMR_D float sd_box(V3 p, V3 c, V3 r) {                                          
 #else
 #define RMR_MB_ATTR __device__ __noinline__
 #endif
+// One iteration of the distance estimator's loop body after the bailout test (r = |z| <= bail):
+// z <- z^power + p0 in spherical form, dr <- power r^(power-1) dr + 1.
+RMR_D void mb_iter(V3& z, float& dr, V3 p0, float power, float r) {
+    float theta = det_acos(z.z / r);
+    float phi = det_atan2(z.y, z.x);
+    // det_pow(r, power - 1) and det_pow(r, power) with their shared det_log(r) computed once,
+    // and sin/cos of one angle from one reduction (det_sincos): the same operations as the
+    // separate calls, so the same bits
+    const float lr = (r == 0.0f) ? 0.0f : det_log(r);
+    const float pm1 = power - 1.0f;
+    const float pw1 = (pm1 == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(pm1 * lr));
+    dr = fmaf(pw1 * power, dr, 1.0f);
+    const float zr = (power == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(power * lr));
+    theta = theta * power;
+    phi = phi * power;
+    float st, ct, sph, cph;
+    det_sincos(theta, st, ct);
+    det_sincos(phi, sph, cph);
+    z = vfma(v3(st * cph, sph * st, ct), zr, p0);
+}
+RMR_D float mb_de(float r, float dr) { return 0.5f * det_log(r) * r / dr; }
 // cnt: the count build's counters (P.counters), nullptr where the caller has none
 RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nullptr) {
     V3 p0 = p - c, z = p0;
@@ -179,24 +200,32 @@ RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nu
         r = length(z);
         if (r > bail) break;
         RMR_COUNT_MB(cnt, active_lanes());   // one iteration of the lanes still iterating
-        float theta = det_acos(z.z / r);
-        float phi = det_atan2(z.y, z.x);
-        // det_pow(r, power - 1) and det_pow(r, power) with their shared det_log(r) computed once,
-        // and sin/cos of one angle from one reduction (det_sincos): the same operations as the
-        // separate calls, so the same bits
-        const float lr = (r == 0.0f) ? 0.0f : det_log(r);
-        const float pm1 = power - 1.0f;
-        const float pw1 = (pm1 == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(pm1 * lr));
-        dr = fmaf(pw1 * power, dr, 1.0f);
-        const float zr = (power == 0.0f) ? 1.0f : ((r == 0.0f) ? 0.0f : det_exp(power * lr));
-        theta = theta * power;
-        phi = phi * power;
-        float st, ct, sph, cph;
-        det_sincos(theta, st, ct);
-        det_sincos(phi, sph, cph);
-        z = vfma(v3(st * cph, sph * st, ct), zr, p0);
+        mb_iter(z, dr, p0, power, r);
     }
-    return 0.5f * det_log(r) * r / dr;
+    return mb_de(r, dr);
+}
+// The same estimator one loop iteration at a time (the stepped map of the scene-specialised kernels,
+// trace_main): a lane's map() spreads over as many wave iterations as its own point needs, instead
+// of every lane of the wave waiting for the slowest one (C3: the bailout count varies per lane).
+// mb_step runs loop iteration s.i; true when the loop is over, with r = the final |z|.
+struct MBStep {
+    V3 z, p0;
+    float dr;
+    int i;         // loop index; -1: no map() in progress
+    V2 pre;        // opU fold of the primitives before the Mandelbulb
+};
+RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, float& r, unsigned long long* cnt) {
+    (void)cnt;
+    if (iters <= 0) {   // the loop does not run: r stays 0
+        r = 0.0f;
+        return true;
+    }
+    r = length(s.z);
+    if (r > bail) return true;
+    RMR_COUNT_MB(cnt, active_lanes());
+    mb_iter(s.z, s.dr, s.p0, power, r);
+    s.i++;
+    return s.i >= iters;
 }
 
 // Register file of a generated function (vec3 vars[total_vars]); indices are wave-uniform.
@@ -742,6 +771,11 @@ struct TableMap {
     static constexpr bool kCache = (NP == -3);
     // the map counts its own executed work (BVH traversals skip primitives; see RMR_COUNT_FLOPS)
     static constexpr bool kCounts = (NP == -2 || NP == -3);
+    // map() one Mandelbulb loop iteration at a time (begin / step / finish: the specialised kernels)
+    static constexpr bool kStepped = false;
+    static RMR_D void begin(const KParams&, V3, MBStep&) {}
+    static RMR_D bool step(const KParams&, MBStep&, float&) { return true; }
+    static RMR_D V2 finish(const KParams& P, V3, const MBStep&, float) { return v2(P.max_dist, -1.0f); }
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
@@ -1540,7 +1574,10 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
-    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
+    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, steps = 0;
+    MBStep mbs;   // stepped map() state (MAP::kStepped)
+    mbs.i = -1;
+    bool maps_done = false;
     constexpr uint32_t CHUNK = RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
@@ -1692,6 +1729,35 @@ RMR_D void trace_main(const KParams& P) {
                 const uint64_t sm = __ballot(is_shade(L.phase));
                 go = RMR_INNER_MARCH && __ballot(is_active(L.phase)) && __popcll(sm) < T;
             }
+        } else if (MAP::kStepped && amask) {
+            // stepped map() (the Mandelbulb one loop iteration per wave iteration): every active lane
+            // runs one estimator iteration per pass; a lane whose estimator finishes completes its
+            // map() (the other primitives and the fold) and applies it, and starts its next map()
+            // in the following pass. Same operations per lane as MAP::eval.
+            uint64_t am = amask;
+            for (;;) {
+                if (is_active(L.phase)) {
+                    if (mbs.i < 0) MAP::begin(P, RMR_MARCH_POINT(L), mbs);
+                    float r;
+                    if (MAP::step(P, mbs, r)) {
+                        if constexpr (!MAP::kCounts)
+                            RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
+                        const V2 m = MAP::finish(P, RMR_MARCH_POINT(L), mbs, r);
+                        mbs.i = -1;
+                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                        else march_update<HO>(P, L, m);
+                        maps_done = true;
+                    }
+                }
+                maps += (uint64_t)__popcll(__ballot(maps_done));
+                maps_done = false;
+                steps += (uint64_t)__popcll(am);
+                iters++;
+                if (!RMR_INNER_MARCH) break;
+                const uint64_t sm = __ballot(is_shade(L.phase));
+                am = __ballot(is_active(L.phase));
+                if (!am || __popcll(sm) >= T) break;
+            }
         } else if (amask) {
             // map() steps back to back until a shading batch is due or no lane is active: idle lanes
             // only appear in shading and refill, so the refill / restart checks can wait until then
@@ -1737,6 +1803,7 @@ RMR_D void trace_main(const KParams& P) {
         atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
         atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
         if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
+        if (MAP::kStepped) atomicAdd(P.counters + 3, (unsigned long long)steps);   // lane-level estimator steps
         atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);

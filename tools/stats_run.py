@@ -31,5 +31,6 @@ lib().rmr_get_counters(r._ctx, raw)
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("RMR_")}, "trace_ms": round(st.trace_ms, 3),
                   "map_evals": st.map_evals, "map_iters": st.map_iters, "shade_batches": st.shade_batches,
                   "lanes_shaded": raw[8], "lanes_per_batch": round(raw[8] / max(1, st.shade_batches), 2),
-                  "evals_per_iter": round(st.map_evals / max(1, st.map_iters), 2)}))
+                  "evals_per_iter": round(st.map_evals / max(1, st.map_iters), 2),
+                  "raw": [int(v) for v in raw]}))
 r.close()
