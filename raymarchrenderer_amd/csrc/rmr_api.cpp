@@ -164,7 +164,11 @@ int upload_bvh(rmr_ctx* c);
 // Escape boxes: each primitive's box for scenes of <= kMaxEscBoxes primitives; for BVH scenes a cut
 // of the hierarchy (the always-visited large primitives individually, then the node with the most
 // primitives split until kMaxEscBoxes boxes). Their union covers every primitive.
-constexpr size_t kMaxEscBoxes = 32;
+constexpr size_t kMaxEscBoxesDefault = 32;
+size_t max_esc_boxes() {   // env RMR_ESC_BOXES (experiments), read at scene upload
+    if (const char* e = std::getenv("RMR_ESC_BOXES")) return (size_t)std::max(1, std::min(64, std::atoi(e)));
+    return kMaxEscBoxesDefault;
+}
 // A Mandelbulb primitive (sd_mandelbulb) takes part when it iterates at least once with a bailout
 // >= 1.5: at |p - c| > bailout its loop stops at once with r = |p - c|, dr = 1, so its distance is
 // 0.5 log(r) r >= 0.30 — the box c +- bailout then bounds everything within 0.001 of it.
@@ -182,6 +186,7 @@ void build_escape_boxes(rmr_ctx* c, bool simple) {
     c->esc_raw.clear();
     bool ok = !s.prims.empty();
     for (const rmr_prim& q : s.prims) ok = ok && escape_prim(q);
+    const size_t kMaxEscBoxes = max_esc_boxes();
     if (!ok || (!simple && s.prims.size() > kMaxEscBoxes)) return;
     auto prim_box = [&](const rmr_prim& q, float* b) {
         for (int k = 0; k < 3; k++) {

@@ -569,8 +569,16 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 // exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere: a sphere is
 // the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) = dot(v,v) for non-NaN v,
 // 0 + S = S) minus its radius; a box subtracts 0 (x - 0 = x). Per-lane index: vector loads.
-RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
-    const float4* q = (const float4*)(P.dprims + k);
+// Where the cached primitives are read from: the leaf-ordered DPrim table itself (global, per-lane
+// vector loads through the L1) or, with RMR_NPC_LDS, a copy of it staged in the workgroup's LDS at
+// kernel start (scenes of <= RMR_NPC_LDS_MAX primitives).
+#ifndef RMR_NPC_LDS
+#define RMR_NPC_LDS 0
+#endif
+#ifndef RMR_NPC_LDS_MAX
+#define RMR_NPC_LDS_MAX 256
+#endif
+RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j) {
     const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type|index<<8 mat_id
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
     const V3 c = v3(a.x, a.y, a.z);
@@ -581,6 +589,9 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
     const V3 qq = vabs(p - c) - h;
     const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
     return (k0 + length(vmax0(qq))) - rad;
+}
+RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
+    return prim_dist_at((const float4*)(P.dprims + k), p, mid, j);
 }
 // Primitives per lane in the nearest-primitive cache (1 or 2): with 2 the cache holds the two
 // nearest primitives and bounds every other one (a ray passing between two neighbours keeps them).
@@ -700,6 +711,9 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         k1 = ks;
     }
     int i = 0;
+#ifdef RMR_NPC_VISITS   // diagnostics: wave-level node tests / prim evaluations vs the per-lane need
+    uint32_t v_tests = 0, v_prims = 0, own_int = 0, own_prims = 0;
+#endif
     while (i < P.n_nodes) {
         const V3 lo = v3(nodes[i].lo[0], nodes[i].lo[1], nodes[i].lo[2]);
         const V3 hi = v3(nodes[i].hi[0], nodes[i].hi[1], nodes[i].hi[2]);
@@ -710,6 +724,11 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         const float ub = fminf(P.max_dist, u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f));
         const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
         const bool need = !(lb2 > t * t);
+#ifdef RMR_NPC_VISITS
+        v_tests++;
+        if (need) { if (nodes[i].count == 0) own_int++; else own_prims += (uint32_t)nodes[i].count; }
+        if (__ballot(need) && nodes[i].count != 0) v_prims += (uint32_t)nodes[i].count;
+#endif
         if (!__ballot(need)) {
             lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
             i = skip;
@@ -733,6 +752,22 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         }
         i = skip;
     }
+    #ifdef RMR_NPC_VISITS
+    {
+        uint32_t mt = 1u + 2u * own_int, mp = own_prims;
+        for (int o = 32; o > 0; o >>= 1) {
+            mt = max(mt, (uint32_t)__shfl_xor((int)mt, o));
+            mp = max(mp, (uint32_t)__shfl_xor((int)mp, o));
+        }
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
+            atomicAdd(P.counters + 4, (unsigned long long)v_tests);
+            atomicAdd(P.counters + 5, (unsigned long long)v_prims);
+            atomicAdd(P.counters + 6, (unsigned long long)mt);
+            atomicAdd(P.counters + 7, (unsigned long long)mp);
+            atomicAdd(P.counters + 9, 1ull);
+        }
+    }
+#endif
     const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
     // no runner-up evaluated (u2 = +inf): every other primitive sits in a skipped node, strictly
     // above the exact minimum (finite u1: a finite point)
@@ -765,6 +800,94 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
     return d;
 }
 
+// map_bvh_npc with a per-lane traversal: every lane walks the pre-order node list with its own
+// culling decisions (the same predicate as the wave-uniform walk, !(lb2 > t^2) with t from the
+// lane's own running minimum), one node test or one primitive per loop pass, so a pass costs one
+// node test plus one primitive whatever the lanes' mix, and the loop runs as long as the busiest
+// lane's own walk instead of the union of every lane's nodes (csg256: ~26 node tests and ~16
+// primitives for the busiest lane against 76 and 81 for the wave-uniform walk, tools/npc_visits.py).
+// Nodes and primitives are per-lane vector loads. The closed form of the fold is order- and
+// subset-free (every skipped primitive is strictly above the minimum), so the map() values are the
+// wave walk's; only the cache outputs (kw, kw2, sb: a lane's own evaluated set) may differ, and
+// those only choose between two exact paths.
+#ifndef RMR_NPC_LANE
+#define RMR_NPC_LANE 0   // csg256 4 spp: 43.2 ms against 36.2 for the wave walk (dependent per-lane loads)
+#endif
+RMR_D V2 map_bvh_npc_lane(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+    const float R2 = P.am_r2;
+    float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff(), lbs = __builtin_inff();
+    int k1 = -1, k2 = -1;
+    if (ks >= 0) {
+        u1 = ds;
+        k1 = ks;
+    }
+    const int n_nodes = P.n_nodes;
+    int i = 0, k = 0, kend = 0;   // next node; pending primitives [k, kend) of the current leaf
+    for (;;) {
+        const bool prim = k < kend;
+        if (!__ballot(prim || i < n_nodes)) break;
+        if (prim) {
+            const float4* q = (const float4*)(P.dprims + k);
+            const float4 a = q[0], b = q[1];   // c.xyz r.x | r.yz type|index<<8 mat_id
+            if (k != ks) {
+                const int type = __float_as_int(b.z) & 0xff;
+                const float av = am_prim(type, p, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y));
+#ifdef RMR_COUNT_FLOPS
+                const uint64_t nb = (uint64_t)__popcll(__ballot(type == RMR_PRIM_BOX));
+                RMR_COUNT(P.counters, nb, 22 + 2, 1);
+                RMR_COUNT(P.counters, active_lanes() - nb, 10 + 2, 1);
+#endif
+                const bool lt1 = av < u1, lt2 = av < u2;
+                u3 = __builtin_amdgcn_fmed3f(u2, av, u3);
+                u2 = __builtin_amdgcn_fmed3f(u1, av, u2);
+                k2 = lt1 ? k1 : (lt2 ? k : k2);
+                k1 = lt1 ? k : k1;
+                u1 = fminf(u1, av);
+            }
+            k++;
+        } else if (i < n_nodes) {
+            const float4* nq = (const float4*)(P.bvh + i);
+            const float4 n0 = nq[0], n1 = nq[1];   // lo.xyz first | hi.xyz count
+            const int skip = __float_as_int(nq[2].x);
+            const V3 q = vmax0(vmax(v3(n0.x, n0.y, n0.z) - p, p - v3(n1.x, n1.y, n1.z)));
+            const float lb2 = dot(q, q);
+            const float ub = fminf(P.max_dist, u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f));
+            const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
+            const int count = __float_as_int(n1.w);
+            if (lb2 > t * t) {
+                lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+                i = skip;
+            } else if (count == 0) {
+                i++;
+            } else {
+                k = __float_as_int(n0.w);
+                kend = k + count;
+                i = skip;
+            }
+        }
+    }
+    const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
+    const bool alone = (u2 == __builtin_inff()) && (u1 < __builtin_inff());
+    const bool uniq = (alone || u2 - u1 > margin) && k1 >= 0;
+    V2 d = v2(P.max_dist, -1.0f);
+    if (uniq) {
+        float mid;
+        int j;
+        const float dw = (k1 == ks) ? ds : prim_dist(P, k1, p, mid, j);
+        if (k1 == ks) mid = ms;
+        opu(d, dw, mid);
+        kw = (dw > P.max_dist) ? -1 : k1;
+        const float v = (RMR_NPC_K >= 2 && k2 >= 0) ? u3 : u2;
+        const float vlb = v - fmaf(fabsf(v) + R2, 0x1p-20f, 0x1p-39f);
+        kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
+        sb = fminf(vlb, lbs);
+    }
+    if (__ballot(!uniq)) {
+        if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);
+    }
+    return d;
+}
+
 template <int NP>
 struct TableMap {
     // NP == -3: the BVH map with the nearest-primitive cache (trace_main's kCache path)
@@ -783,6 +906,7 @@ struct TableMap {
         else return map_general(P, p);
     }
     static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+        if (RMR_NPC_LANE && RMR_NPC_APPROX) return map_bvh_npc_lane(P, p, kw, kw2, sb, ks, js, ds, ms);
         return map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
 };
@@ -1566,6 +1690,9 @@ constexpr int trace_waves() {
 #ifndef RMR_CHUNK
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
+#ifndef RMR_CHUNK_CACHE
+#define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (csg256: +3.7% over 128)
+#endif
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
 #endif
@@ -1578,7 +1705,7 @@ RMR_D void trace_main(const KParams& P) {
     MBStep mbs;   // stepped map() state (MAP::kStepped)
     mbs.i = -1;
     bool maps_done = false;
-    constexpr uint32_t CHUNK = RMR_CHUNK;
+    constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
     bool exhausted = false;
@@ -1596,6 +1723,18 @@ RMR_D void trace_main(const KParams& P) {
 #define RMR_STAMP(v)
 #endif
     __shared__ ChunkRay s_ray[4][CHUNK];   // per wave (256-thread blocks = 4 waves)
+#if RMR_NPC_LDS
+    // the cached primitives' table in LDS (per-lane reads of the cache path)
+    __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
+    const bool dp_lds = MAP::kCache && P.n_prims <= RMR_NPC_LDS_MAX;
+    if (dp_lds) {
+        for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
+        __syncthreads();
+    }
+#define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_at(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
+#else
+#define RMR_PRIM_DIST(k, p, mid, j) prim_dist(P, k, p, mid, j)
+#endif
     const int wv = (threadIdx.x >> 6) & 3;
     uint32_t chunk_base = 0;
     for (;;) {
@@ -1664,14 +1803,14 @@ RMR_D void trace_main(const KParams& P) {
                 int jw = 0;
                 if (act1) {
                     p = RMR_MARCH_POINT(L);
-                    F = prim_dist(P, L.cw, p, mid, jw);
+                    F = RMR_PRIM_DIST(L.cw, p, mid, jw);
                     float Fm = F;
                     if (RMR_NPC_K >= 2) {
                         // both cached primitives, folded in scene order: opU's closed form over the
                         // pair (every other primitive is strictly farther when the bound holds)
                         float mid2;
                         int jw2;
-                        const float F2 = prim_dist(P, L.cw2, p, mid2, jw2);
+                        const float F2 = RMR_PRIM_DIST(L.cw2, p, mid2, jw2);
                         if (jw2 < jw) {
                             opu(m, F2, mid2);
                             opu(m, F, mid);
