@@ -383,6 +383,10 @@ struct BvhItem {
     float lo[3], hi[3], cen[3];
     int idx;
 };
+int bvh_leaf_size() {   // primitives per BVH leaf (env RMR_BVH_LEAF: experiments), read at scene upload
+    if (const char* e = std::getenv("RMR_BVH_LEAF")) return std::max(1, std::min(16, std::atoi(e)));
+    return 8;   // csg256 4 spp: 2 / 3 / 4 / 6 / 8 / 12 / 16 -> 37.0 / 36.1 / 34.1 / 33.3 / 32.9 / 33.1 / 33.6 ms
+}
 void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>& nodes, std::vector<int>& order) {
     const int me = (int)nodes.size();
     nodes.push_back(rmr::BvhNode{});
@@ -396,7 +400,7 @@ void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>
             clo[k] = std::min(clo[k], it[i].cen[k]);
             chi[k] = std::max(chi[k], it[i].cen[k]);
         }
-    if (r - l <= 4) {
+    if (r - l <= bvh_leaf_size()) {
         std::sort(it.begin() + l, it.begin() + r, [](const BvhItem& a, const BvhItem& b) { return a.idx < b.idx; });
         nd.first = (int)order.size();
         nd.count = r - l;

@@ -696,6 +696,9 @@ RMR_D float am_prim(int type, V3 p, V3 c, V3 r) {
 #ifndef RMR_NPC_APPROX
 #define RMR_NPC_APPROX 1
 #endif
+#ifndef RMR_NPC_HOIST
+#define RMR_NPC_HOIST 1
+#endif
 RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
     if (!RMR_NPC_APPROX) return map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
     typedef const __attribute__((address_space(4))) BvhNode CNode;
@@ -710,6 +713,16 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         u1 = ds;
         k1 = ks;
     }
+    // culling radius^2 from the running minimum: a function of u1 alone, so it is recomputed only
+    // where u1 changes (after a leaf); skipped nodes keep only their smallest lb2 (the bound below is
+    // monotonic in it, so one sqrt at the end gives the same lower bound up to v_sqrt's ulp, which
+    // the 1 - 2^-20 factor covers)
+    auto radius2 = [&](float u) {
+        const float ub = fminf(P.max_dist, u + fmaf(fabsf(u) + R2, 0x1p-20f, 0x1p-39f));   // >= the exact minimum
+        const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
+        return t * t;
+    };
+    float t2 = radius2(u1), lbs2 = __builtin_inff();
     int i = 0;
 #ifdef RMR_NPC_VISITS   // diagnostics: wave-level node tests / prim evaluations vs the per-lane need
     uint32_t v_tests = 0, v_prims = 0, own_int = 0, own_prims = 0;
@@ -720,17 +733,15 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
         const int count = nodes[i].count, skip = nodes[i].skip;
         const V3 q = vmax0(vmax(lo - p, p - hi));
         const float lb2 = dot(q, q);
-        // >= the exact running minimum (capped at maxDist as the exact fold's dbest)
-        const float ub = fminf(P.max_dist, u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f));
-        const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
-        const bool need = !(lb2 > t * t);
+        const bool need = !(lb2 > (RMR_NPC_HOIST ? t2 : radius2(u1)));
 #ifdef RMR_NPC_VISITS
         v_tests++;
         if (need) { if (nodes[i].count == 0) own_int++; else own_prims += (uint32_t)nodes[i].count; }
         if (__ballot(need) && nodes[i].count != 0) v_prims += (uint32_t)nodes[i].count;
 #endif
         if (!__ballot(need)) {
-            lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+            if (RMR_NPC_HOIST) lbs2 = fminf(lbs2, lb2);
+            else lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
             i = skip;
             continue;
         }
@@ -750,8 +761,10 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
             k1 = lt1 ? k : k1;
             u1 = fminf(u1, a);
         }
+        if (RMR_NPC_HOIST) t2 = radius2(u1);
         i = skip;
     }
+    if (RMR_NPC_HOIST) lbs = fmaf(__builtin_amdgcn_sqrtf(lbs2), 1.0f - 0x1p-20f, -P.bvh_margin);
     #ifdef RMR_NPC_VISITS
     {
         uint32_t mt = 1u + 2u * own_int, mp = own_prims;
