@@ -62,6 +62,28 @@ static float sd_box(o_v3 p, o_v3 c, o_v3 r) {
     o_v3 q = v_sub(v_abs(v_sub(p, c)), r);
     return fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f) + v_length(v_max0(q));
 }
+/* power 8 without transcendentals (csrc/rmr_trace.h mb_iter8, the same operations): cos/sin of
+ * theta = acos(z.z/r) and phi = atan2(z.y, z.x) from the components, 8 theta / 8 phi by three angle
+ * doublings, r^8 and r^7 by products */
+static void mb_iter8(o_v3* z, float* dr, o_v3 p0, float r) {
+    float ct = z->z / r;
+    float st = sqrtf(fmaxf(fmaf(-ct, ct, 1.0f), 0.0f));
+    const float rho2 = fmaf(z->x, z->x, z->y * z->y);
+    float cp = 1.0f, sp = 0.0f;
+    if (rho2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(rho2);
+        cp = z->x * inv;
+        sp = z->y * inv;
+    }
+    for (int k = 0; k < 3; k++) {
+        const float st2 = (2.0f * st) * ct, ct2 = fmaf(ct, ct, -(st * st));
+        const float sp2 = (2.0f * sp) * cp, cp2 = fmaf(cp, cp, -(sp * sp));
+        st = st2; ct = ct2; sp = sp2; cp = cp2;
+    }
+    const float r2 = r * r, r4 = r2 * r2, r8 = r4 * r4, r7 = (r4 * r2) * r;
+    *dr = fmaf(8.0f * r7, *dr, 1.0f);
+    *z = v_fma(o3(st * cp, sp * st, ct), r8, p0);
+}
 /* map_mandelbulb — new node: power-N bulb, distance 0.5*log(r)*r/dr */
 static float sd_mandelbulb(o_v3 p, o_v3 c, o_v3 prm) {
     o_v3 p0 = v_sub(p, c);
@@ -72,6 +94,10 @@ static float sd_mandelbulb(o_v3 p, o_v3 c, o_v3 prm) {
     for (int i = 0; i < iters; i++) {
         r = v_length(z);
         if (r > bail) break;
+        if (power == 8.0f) {
+            mb_iter8(&z, &dr, p0, r);
+            continue;
+        }
         float theta = det_acos(z.z / r);
         float phi = det_atan2(z.y, z.x);
         dr = fmaf(det_pow(r, power - 1.0f) * power, dr, 1.0f);

@@ -111,10 +111,13 @@ RMR_D void count_work(unsigned long long* cnt, uint64_t lanes, uint64_t flops_pe
     }
 }
 #define RMR_COUNT(cnt, lanes, f, t) count_work((cnt), (lanes), (f), (t))
-#define RMR_COUNT_MB(cnt, lanes) count_work((cnt), (lanes), 27, 10, 27)
+// Mandelbulb iteration: 27 flops + 10 transcendentals (trigonometric form), 59 flops + 2 square
+// roots (power 8, mb_iter8)
+#define RMR_COUNT_MB(cnt, lanes, power) \
+    ((power) == 8.0f ? count_work((cnt), (lanes), 59, 2, 59) : count_work((cnt), (lanes), 27, 10, 27))
 #else
 #define RMR_COUNT(cnt, lanes, f, t) ((void)0)
-#define RMR_COUNT_MB(cnt, lanes) ((void)0)
+#define RMR_COUNT_MB(cnt, lanes, power) ((void)0)
 #endif
 RMR_D uint64_t active_lanes() { return (uint64_t)__popcll(__ballot(1)); }
 
@@ -168,9 +171,39 @@ RMR_D float sd_box(V3 p, V3 c, V3 r) {                                          
 #else
 #define RMR_MB_ATTR __device__ __noinline__
 #endif
+// Power 8 without transcendentals: z^8 in the same spherical form, with cos/sin of
+// theta = acos(z.z / r) and of phi = atan2(z.y, z.x) taken from the components (sin theta >= 0 as
+// acos's range gives; phi = 0 on the z axis, as atan2(0, 0)) and 8 theta, 8 phi by three angle
+// doublings (sin 2a = 2 sin a cos a, cos 2a = cos^2 a - sin^2 a), r^8 and r^7 by products. The same
+// function as the trigonometric iteration below, rounded differently (oracle/rmr_oracle.c states
+// the identical operations; the llvmpipe golden of the trigonometric GLSL statement pins it by PSNR).
+RMR_D void mb_iter8(V3& z, float& dr, V3 p0, float r) {
+    float ct = z.z / r;
+    float st = sqrt_cr(fmaxf(fmaf(-ct, ct, 1.0f), 0.0f));
+    const float rho2 = fmaf(z.x, z.x, z.y * z.y);
+    float cp = 1.0f, sp = 0.0f;
+    if (rho2 > 0.0f) {
+        const float inv = 1.0f / sqrt_cr(rho2);
+        cp = z.x * inv;
+        sp = z.y * inv;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float st2 = (2.0f * st) * ct, ct2 = fmaf(ct, ct, -(st * st));
+        const float sp2 = (2.0f * sp) * cp, cp2 = fmaf(cp, cp, -(sp * sp));
+        st = st2; ct = ct2; sp = sp2; cp = cp2;
+    }
+    const float r2 = r * r, r4 = r2 * r2, r8 = r4 * r4, r7 = (r4 * r2) * r;
+    dr = fmaf(8.0f * r7, dr, 1.0f);
+    z = vfma(v3(st * cp, sp * st, ct), r8, p0);
+}
 // One iteration of the distance estimator's loop body after the bailout test (r = |z| <= bail):
 // z <- z^power + p0 in spherical form, dr <- power r^(power-1) dr + 1.
 RMR_D void mb_iter(V3& z, float& dr, V3 p0, float power, float r) {
+    if (power == 8.0f) {
+        mb_iter8(z, dr, p0, r);
+        return;
+    }
     float theta = det_acos(z.z / r);
     float phi = det_atan2(z.y, z.x);
     // det_pow(r, power - 1) and det_pow(r, power) with their shared det_log(r) computed once,
@@ -199,7 +232,7 @@ RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nu
     for (int i = 0; i < iters; i++) {
         r = length(z);
         if (r > bail) break;
-        RMR_COUNT_MB(cnt, active_lanes());   // one iteration of the lanes still iterating
+        RMR_COUNT_MB(cnt, active_lanes(), power);   // one iteration of the lanes still iterating
         mb_iter(z, dr, p0, power, r);
     }
     return mb_de(r, dr);
@@ -222,7 +255,7 @@ RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, float& r, unsi
     }
     r = length(s.z);
     if (r > bail) return true;
-    RMR_COUNT_MB(cnt, active_lanes());
+    RMR_COUNT_MB(cnt, active_lanes(), power);
     mb_iter(s.z, s.dr, s.p0, power, r);
     s.i++;
     return s.i >= iters;

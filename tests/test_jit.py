@@ -371,3 +371,26 @@ def test_split_schedule_multichunk_vs_oracle(renderer):
     cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).render(times)
     same = (gpu.view(np.uint32) == cpu.view(np.uint32)) | (np.isnan(gpu) & np.isnan(cpu))
     assert same.all(), "%d values differ" % (~same).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("step", ["0", "1"])
+def test_mandelbulb_stepped_map_bitexact_vs_oracle(renderer, monkeypatch, step):
+    """The opt-in stepped Mandelbulb map (RMR_JIT_STEP=1, rmr_trace.h MBStep: one estimator iteration
+    per lane per wave pass) and the whole-map default both equal the oracle sample for sample."""
+    monkeypatch.setenv("RMR_JIT_STEP", step)
+    path = os.path.join(SCENES, "mandelbulb.scene")
+    W, H = 48, 40
+    rect = (0, 0, W, H)
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 2})
+    renderer.set_jit(1)
+    try:
+        times = time_schedule(2, frame=4)
+        gpu = renderer.trace_samples(times, rect)
+        assert renderer.stats().jit_launches > 0
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "RMR_JIT_STEP=%s: %d samples differ" % (step, (~same.all(-1)).sum())
