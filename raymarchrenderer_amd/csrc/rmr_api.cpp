@@ -196,7 +196,7 @@ void build_escape_boxes(rmr_ctx* c, bool simple) {
         }
     };
     float b[6];
-    if (c->map_np != -2) {
+    if (c->map_np != -2 || s.prims.size() <= kMaxEscBoxes) {   // one box per primitive
         for (const rmr_prim& q : s.prims) {
             prim_box(q, b);
             c->esc_raw.insert(c->esc_raw.end(), b, b + 6);
@@ -250,30 +250,6 @@ int upload_scene(rmr_ctx* c) {
     if ((r = dev_upload(c, &c->d_mats, s.materials.data(), s.materials.size()))) return r;
     if ((r = dev_upload(c, &c->d_spec, s.spectral.data(), s.spectral.size()))) return r;
     if ((r = dev_upload(c, &c->d_rm2, &s.rm2, 1))) return r;
-    // packed prims + map() specialisation
-    bool simple = true;
-    for (const auto& p : s.prims) simple = simple && (p.type == RMR_PRIM_SPHERE || p.type == RMR_PRIM_BOX);
-    const size_t n = s.prims.size();
-    c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : (n <= kMaxLoopPrims ? 0 : -2)));
-    if (c->map_np == -2) {
-        if ((r = upload_bvh(c))) return r;
-    } else {
-        std::vector<rmr::DPrim> dp(std::max<size_t>(n, 8));
-        for (size_t i = 0; i < dp.size(); i++) {
-            rmr::DPrim q{};
-            if (i < n) {
-                const rmr_prim& p = s.prims[i];
-                for (int k = 0; k < 3; k++) { q.c[k] = p.c[k]; q.r[k] = p.r[k]; }
-                q.type = p.type;
-                q.mat_id = p.mat_id;
-            }
-            dp[i] = q;
-        }
-        if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
-        c->n_bvh = 0;
-    }
-    build_escape_boxes(c, simple);
-    c->esc_infl_dev = -1.0;
     // shading kinds (RM1): recognise the single-node diffuse / emission materials
     std::vector<rmr::DMat> dm(std::max<size_t>(1, s.materials.size()));
     for (size_t i = 0; i < s.materials.size(); i++) {
@@ -305,6 +281,31 @@ int upload_scene(rmr_ctx* c) {
     c->has_prog = false;
     for (const auto& d : dm) c->has_prog = c->has_prog || d.kind == rmr::MAT_PROGRAM;
     if ((r = dev_upload(c, &c->d_dmats, dm.data(), dm.size()))) return r;
+    // packed prims + map() specialisation
+    bool simple = true;
+    for (const auto& p : s.prims) simple = simple && (p.type == RMR_PRIM_SPHERE || p.type == RMR_PRIM_BOX);
+    const size_t n = s.prims.size();
+    c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : (n <= kMaxLoopPrims ? 0 : -2)));
+    if (c->map_np >= 0 && rmr::small_npc_applies(s, c->has_prog, c->cull)) c->map_np = -2;   // (see rmr_jit.hpp)
+    if (c->map_np == -2) {
+        if ((r = upload_bvh(c))) return r;
+    } else {
+        std::vector<rmr::DPrim> dp(std::max<size_t>(n, 8));
+        for (size_t i = 0; i < dp.size(); i++) {
+            rmr::DPrim q{};
+            if (i < n) {
+                const rmr_prim& p = s.prims[i];
+                for (int k = 0; k < 3; k++) { q.c[k] = p.c[k]; q.r[k] = p.r[k]; }
+                q.type = p.type;
+                q.mat_id = p.mat_id;
+            }
+            dp[i] = q;
+        }
+        if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
+        c->n_bvh = 0;
+    }
+    build_escape_boxes(c, simple);
+    c->esc_infl_dev = -1.0;
     c->scene_loaded = true;
     c->jit_ready = false;
     c->jit_failed = false;

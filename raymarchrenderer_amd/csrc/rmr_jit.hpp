@@ -27,6 +27,12 @@ struct JitKernel {
 };
 // Workgroup size of the split kernels (rmr_trace.h trace_split: RMR_SPLIT_WAVES waves)
 constexpr int kSplitBlock = 512;
+// Small sphere/box scenes (<= 32 primitives) through the nearest-primitive cache (a one-leaf BVH in
+// the table, TableMap<-3> in the kernel) instead of the straight-line approximate map: env
+// RMR_SMALL_NPC (1: two cached primitives, 2: one), HO kernels with RMR_CULL_NPC only.
+int small_npc_mode();
+bool small_npc_applies(const CompiledScene& s, bool prog, int cull);
+
 // The split schedule applies to this specialisation (HO kernel without the nearest-primitive cache)
 bool jit_split_applies(const CompiledScene& s, bool prog, int cull);
 

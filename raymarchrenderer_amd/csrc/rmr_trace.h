@@ -599,9 +599,11 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 }
 #define NPC_PROBE_DELTA 0.0010001f
 #define NPC_BOUNCE_DELTA 0.0031f
-// exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere: a sphere is
-// the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) = dot(v,v) for non-NaN v,
-// 0 + S = S) minus its radius; a box subtracts 0 (x - 0 = x). Per-lane index: vector loads.
+// exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere at points
+// without NaN: a sphere is the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) =
+// dot(v,v) for non-NaN v, 0 + S = S) minus its radius; a box subtracts 0 (x - 0 = x). (At a NaN
+// point fmaxf / fminf drop the NaN: a sphere then gives -r where sd_sphere gives NaN.) Per-lane
+// index: vector loads.
 // Where the cached primitives are read from: the leaf-ordered DPrim table itself (global, per-lane
 // vector loads through the L1) or, with RMR_NPC_LDS, a copy of it staged in the workgroup's LDS at
 // kernel start (scenes of <= RMR_NPC_LDS_MAX primitives).
@@ -1847,6 +1849,7 @@ RMR_D void trace_main(const KParams& P) {
                 bool ok = false;
                 float F = 0.0f, mid = -1.0f;
                 int jw = 0;
+                bool pfin = false;   // a point without NaN (and without +-inf of both signs)
                 if (act1) {
                     p = RMR_MARCH_POINT(L);
                     F = RMR_PRIM_DIST(L.cw, p, mid, jw);
@@ -1881,7 +1884,8 @@ RMR_D void trace_main(const KParams& P) {
 #endif
                     const float delta = (L.phase == PH_NORMAL) ? NPC_PROBE_DELTA : (L.t - L.cta) * (1.0f + 0x1p-21f);
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
-                    ok = (sum == sum) && (L.cs - delta - npc_eps(P, p) > Fm);
+                    pfin = sum == sum;
+                    ok = pfin && (L.cs - delta - npc_eps(P, p) > Fm);
                 }
                 const uint64_t okm = __ballot(act1 && ok);
                 const uint64_t fm = __ballot(act1 && !ok);
@@ -1892,7 +1896,9 @@ RMR_D void trace_main(const KParams& P) {
                     if (act1 && !ok) {
                         int kw, kw2;
                         float s2;
-                        m = MAP::full(P, p, kw, kw2, s2, F == F ? L.cw : -1, jw, F, mid);
+                        // seeded with the cached primitive only at a finite point: prim_dist's box form
+                        // of a sphere drops a NaN coordinate (fmaxf / fminf) where sd_sphere keeps it
+                        m = MAP::full(P, p, kw, kw2, s2, (pfin && F == F) ? L.cw : -1, jw, F, mid);
                         L.cw = kw >= 0 ? kw : 0;
                         L.cw2 = kw >= 0 ? kw2 : 0;
                         // |s2| 2^-20: the rounding of the check's own subtractions
@@ -1904,6 +1910,16 @@ RMR_D void trace_main(const KParams& P) {
                     }
                     fulls++;
                 }
+#ifdef RMR_NPC_CHECK   // diagnostics (RMR_JIT_OPTS=-DRMR_NPC_CHECK): every cached map() against the exact fold
+                if (done) {
+                    const V2 ex = map_bvh(P, p);
+                    if (__float_as_uint(ex.x) != __float_as_uint(m.x) || __float_as_uint(ex.y) != __float_as_uint(m.y))
+                        printf("NPC mismatch unit %u ph %d ctr %d t %a cta %a p (%a %a %a) m (%a %a) exact (%a %a) ok %d "
+                               "cw %d cw2 %d F %a cs %a\n",
+                               L.unit, L.phase, L.ctr, L.t, L.cta, p.x, p.y, p.z, m.x, m.y, ex.x, ex.y, (int)ok, L.cw, L.cw2,
+                               F, L.cs);
+                }
+#endif
                 if (done) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO, true>(P, L, m);

@@ -251,6 +251,48 @@ def test_shelf_nan_directions_bitexact_vs_oracle(renderer):
     assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
 
 
+def _bvh_cornell_scene():
+    """Cornell-5 padded past the inline-map limit with 30 small spheres far above the box (no map()
+    value changes: they never attain the minimum), so it runs through the BVH map with the
+    nearest-primitive cache."""
+    import json
+    with open(os.path.join(SCENES, "cornell5.scene")) as f:
+        sc = json.load(f)
+    ball = sc["objects"][3]
+    for n in range(30):
+        pad = json.loads(json.dumps(ball))
+        pad["nodes"][0]["inputs"][1] = [-3.0 + 0.2 * n, 9.0 + 0.1 * (n % 3), -2.0 + 0.13 * n]
+        pad["nodes"][0]["inputs"][2] = [0.05, 0.05, 0.05]
+        sc["objects"].append(pad)
+    return sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [1, 0])
+def test_bvh_cache_nan_point_with_cached_sphere_bitexact(renderer, jit):
+    """A NaN bounce direction (randHemisphere about a getNormal of exactly (0,-1,0), here the
+    sphere's bottom) while the lane's cached primitive is the sphere: the cached distance at the NaN
+    point is not NaN (prim_dist's box form drops NaN coordinates), so it must not seed the full map.
+    Sample 3 of pixel (1441, 652) of the 1080p C2 view took that path (found at full frame: one
+    sample in 8.3 M rendered the wrong path before the fix)."""
+    sc = _bvh_cornell_scene()
+    W, H = 1920, 1080
+    rect = (1440, 648, 1448, 656)
+    prm, view = _setup(renderer, sc, "rm1", W, H, {"max_bounces": 4})
+    renderer.set_jit(jit)
+    try:
+        renderer.reset_stats()
+        times = time_schedule(4)
+        gpu = renderer.trace_samples(times, rect)
+        assert (renderer.stats().jit_launches > 0) == (jit == 1)
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(scene_compile.compile_scene(sc, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12),
                                                ("mandelbulb.scene", 2, 2), ("rm3", 16, 8)])
