@@ -15,6 +15,7 @@
 #include <new>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rmr.h"
@@ -73,6 +74,12 @@ struct rmr_ctx {
     int env_w = 0, env_h = 0;
     int n_bvh = 0;
     float bvh_margin = 1e-4f;
+    // candidate grid of the cache's full map() (build_grid; BVH scenes)
+    uint2* d_grid = nullptr;
+    uint16_t* d_grid_list = nullptr;
+    bool grid_on = false;
+    float grid_lo[3] = {0, 0, 0}, grid_inv = 1.0f;
+    int grid_dim[3] = {0, 0, 0}, grid_n_large = 0;
     int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
     bool has_prog = true;  // RM1 scene has materials needing the generic node interpreter
     // buffers
@@ -94,7 +101,9 @@ struct rmr_ctx {
     int shade_threshold = 16;   // explicit (env RMR_SHADE_T / rmr_set_tuning) or, with shade_auto, per kernel:
     bool shade_auto = true;     // per specialised kernel (ensure_jit: 20 / 8 / 16), 16 for the table kernels
     int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
-    int full_threshold = 40 | (2 << 8);   // nearest-primitive cache: 40 lanes per full map() batch, R = 2 (csg256)
+    // nearest-primitive cache: 40 lanes per full map() batch, or once waiting lanes >= cache-served ones
+    // (R = 8; csg256 with the candidate grid: 15.7 -> 14.8 ms per 4 spp against R = 2)
+    int full_threshold = 40 | (8 << 8);
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
     int sched = RMR_SCHED_MEGA;    // rmr_set_schedule
     int grid_per_cu = 0;  // 0 = occupancy
@@ -303,9 +312,14 @@ int upload_scene(rmr_ctx* c) {
         }
         if ((r = dev_upload(c, &c->d_dprims, dp.data(), dp.size()))) return r;
         c->n_bvh = 0;
+        c->grid_on = false;
     }
     build_escape_boxes(c, simple);
     c->esc_infl_dev = -1.0;
+    if (const char* e = std::getenv("RMR_FULL_T"))   // (experiments; read per scene load)
+        c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RMR_FULL_R"))
+        c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
     c->scene_loaded = true;
     c->jit_ready = false;
     c->jit_failed = false;
@@ -330,7 +344,10 @@ int ensure_jit(rmr_ctx* c) {
     }
     c->jit_struct_src = struct_src;
     const bool split = c->sched == RMR_SCHED_SPLIT && rmr::jit_split_applies(c->scene, c->has_prog, c->cull);
-    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, split);
+    // one cached primitive when the cache's full map() runs through the candidate grid (csg256: 21.5 ->
+    // 17.4 ms per 4 spp against two); two with the BVH full map
+    const int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, split, npc_k);
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {
@@ -423,6 +440,169 @@ void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>
 }
 }  // namespace
 
+// Candidate grid over the small primitives (leaf order [n_large, n)) of a BVH scene, for the nearest-
+// primitive cache's full map() (rmr_trace.h map_grid_npc). Per cell C (inflated past the kernel's
+// rounding of the cell index): U = the smallest distance upper bound over C of any primitive (box and
+// sphere SDFs are convex: the maximum is at a corner); the list = the small primitives whose distance
+// lower bound over C is <= U + margin (margin = 4 x the float evaluation error bound of a distance
+// anywhere in the grid, so an unlisted primitive's float distance is strictly above the minimum's);
+// the cell's bound = the smallest lower bound of an unlisted one, minus that error bound. Exact
+// arithmetic in double; cells of more than 254 candidates keep the BVH (count 255).
+// Env (experiments): RMR_GRID=0 off, RMR_GRID_CELLS (target cell count), RMR_GRID_PAD (cells).
+int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, double E) {
+    c->grid_on = false;
+    if (const char* e = std::getenv("RMR_GRID")) if (std::atoi(e) == 0) return RMR_OK;
+    const int n = (int)dp.size();
+    if (n - n_large < 1 || n > 65535) return RMR_OK;
+    auto half = [&](const rmr::DPrim& q, int k) {
+        return (double)std::fabs((q.type & 0xff) == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]);
+    };
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int i = n_large; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], (double)dp[(size_t)i].c[k] - half(dp[(size_t)i], k));
+            hi[k] = std::max(hi[k], (double)dp[(size_t)i].c[k] + half(dp[(size_t)i], k));
+        }
+    // the region: the small primitives' box grown by pad x its largest extent on every side, clipped
+    // to the box of all primitives (large ones included) grown by one cell
+    double target = 262144.0, pad = 0.5;
+    if (const char* e = std::getenv("RMR_GRID_CELLS")) target = std::max(1.0, std::atof(e));
+    if (const char* e = std::getenv("RMR_GRID_PAD")) pad = std::max(0.0, std::atof(e));
+    double alo[3] = {1e300, 1e300, 1e300}, ahi[3] = {-1e300, -1e300, -1e300};
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            alo[k] = std::min(alo[k], (double)dp[(size_t)i].c[k] - half(dp[(size_t)i], k));
+            ahi[k] = std::max(ahi[k], (double)dp[(size_t)i].c[k] + half(dp[(size_t)i], k));
+        }
+    const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    double rlo[3], rhi[3];
+    for (int k = 0; k < 3; k++) {
+        rlo[k] = lo[k] - pad * ext;
+        rhi[k] = hi[k] + pad * ext;
+    }
+    double cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
+    for (int k = 0; k < 3; k++) {
+        rlo[k] = std::max(rlo[k], alo[k] - cs);
+        rhi[k] = std::min(rhi[k], ahi[k] + cs);
+    }
+    cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
+    for (int k = 0; k < 3; k++) cs = std::max(cs, (rhi[k] - rlo[k]) / 1024.0);
+    if (!(cs > 0.0) || !std::isfinite(cs)) return RMR_OK;
+    int dim[3];
+    float flo[3];
+    double pmax = E;
+    for (int k = 0; k < 3; k++) {
+        flo[k] = (float)rlo[k];
+        dim[k] = std::max(1, (int)std::ceil((rhi[k] - (double)flo[k]) / cs));
+        pmax = std::max(pmax, std::max(std::fabs((double)flo[k]), std::fabs((double)flo[k] + dim[k] * cs)));
+    }
+    const float finv = (float)(1.0 / cs);
+    const double csf = 1.0 / (double)finv;   // the cell size the kernel's index arithmetic implies
+    const size_t ncell = (size_t)dim[0] * dim[1] * dim[2];
+    if (ncell > ((size_t)1 << 24)) return RMR_OK;
+    // float error bound of a box/sphere distance at |p|_inf <= pmax (rmr_trace.h npc_eps, 4x slack)
+    const double eps = std::ldexp(pmax + E, -17);
+    const double margin = 4.0 * eps;
+    const double infl = 1e-4 + std::ldexp(pmax, -16) + 4.0 * std::ldexp(csf, -20);   // cell index rounding
+    struct PB { double c[3], h[3], rad; bool box; };
+    std::vector<PB> pb((size_t)n);
+    for (int i = 0; i < n; i++) {
+        const rmr::DPrim& q = dp[(size_t)i];
+        PB b{};
+        b.box = (q.type & 0xff) == RMR_PRIM_BOX;
+        for (int k = 0; k < 3; k++) { b.c[k] = q.c[k]; b.h[k] = b.box ? (double)q.r[k] : 0.0; }
+        b.rad = b.box ? 0.0 : (double)q.r[0];
+        pb[(size_t)i] = b;
+    }
+    // distance bounds of primitive b over the cell [a0, a1]: lower (Euclidean distance to the box of
+    // half-extent |h| minus the radius; -min|h| - rad when they overlap) and upper (the largest corner value)
+    auto bounds = [&](const PB& b, const double* a0, const double* a1, double& dmin, double& dmax) {
+        double s2 = 0.0, f2 = 0.0, mh = 1e300;
+        bool overlap = true;
+        for (int k = 0; k < 3; k++) {
+            const double h = std::fabs(b.h[k]);
+            const double gap = std::max({a0[k] - (b.c[k] + h), (b.c[k] - h) - a1[k], 0.0});
+            if (gap > 0.0) overlap = false;
+            s2 += gap * gap;
+            mh = std::min(mh, h);
+        }
+        dmin = overlap ? (b.box ? -mh : -b.rad) : std::sqrt(s2) - b.rad;
+        dmax = -1e300;
+        for (int corner = 0; corner < 8; corner++) {
+            double qv[3], mq = -1e300, o2 = 0.0;
+            for (int k = 0; k < 3; k++) {
+                const double x = (corner >> k) & 1 ? a1[k] : a0[k];
+                qv[k] = std::fabs(x - b.c[k]) - b.h[k];
+                mq = std::max(mq, qv[k]);
+                o2 += std::max(qv[k], 0.0) * std::max(qv[k], 0.0);
+            }
+            (void)f2;
+            dmax = std::max(dmax, std::min(mq, 0.0) + std::sqrt(o2) - b.rad);
+        }
+    };
+    std::vector<std::vector<uint16_t>> lists(ncell);
+    std::vector<uint32_t> cnt(ncell);
+    std::vector<float> lout(ncell);
+    auto work = [&](int z0, int z1) {
+        std::vector<double> dmn((size_t)n), dmx((size_t)n);
+        for (int z = z0; z < z1; z++)
+            for (int y = 0; y < dim[1]; y++)
+                for (int x = 0; x < dim[0]; x++) {
+                    const int ii[3] = {x, y, z};
+                    double a0[3], a1[3];
+                    for (int k = 0; k < 3; k++) {
+                        a0[k] = (double)flo[k] + ii[k] * csf - infl;
+                        a1[k] = (double)flo[k] + (ii[k] + 1) * csf + infl;
+                    }
+                    double U = 1e300;
+                    for (int i = 0; i < n; i++) {
+                        bounds(pb[(size_t)i], a0, a1, dmn[(size_t)i], dmx[(size_t)i]);
+                        U = std::min(U, dmx[(size_t)i]);
+                    }
+                    const size_t ci = ((size_t)z * dim[1] + y) * dim[0] + x;
+                    double lo_out = 1e300;
+                    std::vector<uint16_t>& L = lists[ci];
+                    for (int i = n_large; i < n; i++) {
+                        if (dmn[(size_t)i] <= U + margin) L.push_back((uint16_t)i);
+                        else lo_out = std::min(lo_out, dmn[(size_t)i]);
+                    }
+                    if (L.size() > 254) { cnt[ci] = 255; L.clear(); }
+                    else cnt[ci] = (uint32_t)L.size();
+                    float lf = lo_out >= 1e300 ? HUGE_VALF : (float)(lo_out - eps);
+                    if ((double)lf > lo_out - eps) lf = std::nextafter(lf, -HUGE_VALF);
+                    lout[ci] = lf;
+                }
+    };
+    {
+        const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        const int per = (dim[2] + nt - 1) / nt;
+        for (int t = 0; t < nt; t++) {
+            const int z0 = t * per, z1 = std::min(dim[2], z0 + per);
+            if (z0 < z1) th.emplace_back(work, z0, z1);
+        }
+        for (auto& t : th) t.join();
+    }
+    std::vector<uint2> cells(ncell);
+    std::vector<uint16_t> flat;
+    for (size_t i = 0; i < ncell; i++) {
+        if (flat.size() + lists[i].size() >= ((size_t)1 << 24)) return RMR_OK;
+        cells[i].x = (uint32_t)flat.size() | (cnt[i] << 24);
+        uint32_t lb;
+        std::memcpy(&lb, &lout[i], 4);
+        cells[i].y = lb;
+        flat.insert(flat.end(), lists[i].begin(), lists[i].end());
+    }
+    int r;
+    if ((r = dev_upload(c, &c->d_grid, cells.data(), cells.size()))) return r;
+    if ((r = dev_upload(c, &c->d_grid_list, flat.data(), flat.size()))) return r;
+    for (int k = 0; k < 3; k++) { c->grid_lo[k] = flo[k]; c->grid_dim[k] = dim[k]; }
+    c->grid_inv = finv;
+    c->grid_n_large = n_large;
+    c->grid_on = true;
+    return RMR_OK;
+}
+
 int upload_bvh(rmr_ctx* c) {
     const CompiledScene& s = c->scene;
     std::vector<BvhItem> items;
@@ -480,7 +660,18 @@ int upload_bvh(rmr_ctx* c) {
     c->bvh_order = order;
     c->n_bvh = (int)nodes.size();
     c->bvh_margin = 1e-4f + extent * 0x1p-16f;
-    return RMR_OK;
+    double E = 0.0;   // max |c|_inf + |r|_inf (as render_tiles' npc_eps0)
+    for (const rmr_prim& q : s.prims) {
+        const double rr = q.type == RMR_PRIM_SPHERE ? std::fabs(q.r[0])
+                                                    : std::max({std::fabs(q.r[0]), std::fabs(q.r[1]), std::fabs(q.r[2])});
+        E = std::max(E, std::max({std::fabs((double)q.c[0]), std::fabs((double)q.c[1]), std::fabs((double)q.c[2])}) + rr);
+    }
+    int n_large = 0;
+    for (const rmr::BvhNode& nd : nodes) {   // the always-visited leaves come first (leaf order 0 ..)
+        if (nd.lo[0] > -1e38f) break;
+        n_large += nd.count;
+    }
+    return build_grid(c, dp, n_large, E);
 }
 
 int validate_scene(rmr_ctx* c, const CompiledScene& s) {
@@ -593,6 +784,10 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.spec = c->d_spec; P.rm2 = c->d_rm2;
     P.dprims = c->d_dprims; P.dmats = c->d_dmats;
     P.bvh = c->d_bvh; P.n_nodes = c->n_bvh; P.bvh_margin = c->bvh_margin;
+    if (c->grid_on && c->map_np == -2) {
+        P.grid = c->d_grid; P.grid_list = c->d_grid_list; P.grid_inv = c->grid_inv; P.grid_n_large = c->grid_n_large;
+        for (int k = 0; k < 3; k++) { P.grid_lo[k] = c->grid_lo[k]; P.grid_dim[k] = c->grid_dim[k]; }
+    }
     P.n_prims = (int)s.prims.size();
     P.am_r2 = 2.0f * rmr::max_sphere_radius(s);
     {
@@ -768,10 +963,6 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
     if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
     if (const char* e = std::getenv("RMR_SPLIT")) c->sched = std::atoi(e) ? RMR_SCHED_SPLIT : RMR_SCHED_MEGA;
-    if (const char* e = std::getenv("RMR_FULL_T"))
-        c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RMR_FULL_R"))
-        c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
@@ -786,7 +977,7 @@ void rmr_destroy(rmr_ctx* c) {
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
     void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_esc, c->d_env, c->d_samp,
-                    c->d_tiles, c->d_times, c->d_queue, c->d_counters, c->d_srgb_thr, c->d_screen};
+                    c->d_tiles, c->d_times, c->d_queue, c->d_counters, c->d_srgb_thr, c->d_screen, c->d_grid, c->d_grid_list};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);

@@ -58,6 +58,16 @@ struct KParams {
     const DMat* dmats;          // per-id shading kind (RM1)
     const BvhNode* bvh;         // NP = -2: node array (n_nodes), prims in dprims in leaf order
     int32_t n_nodes;
+    // candidate grid of the nearest-primitive cache's full map() (rmr_trace.h map_grid_npc; null =
+    // none): per cell x = list offset | count << 24 (count 255: no list, take the BVH), y = float bits
+    // of a lower bound of every non-listed primitive's float distance in the cell; lists of leaf
+    // indices; leaf indices [0, grid_n_large) are evaluated everywhere (large primitives)
+    const uint2* grid;
+    const uint16_t* grid_list;
+    float grid_lo[3];
+    float grid_inv;             // 1 / cell size
+    int32_t grid_dim[3];
+    int32_t grid_n_large;
     float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)
     float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     float npc_eps0;             // nearest-primitive cache: 2^-17 E + 2^-60 (rmr_trace.h npc_eps)

@@ -44,8 +44,9 @@ bool jit_split_applies(const CompiledScene& s, bool prog, int cull);
 // live (with bake): primitives j with live[j] != 0 are loaded even so (an animation's moving
 // primitives; the rest stay literals).
 // split: the march / shade split schedule where it applies (jit_split_applies).
+// npc_k: primitives per lane in the nearest-primitive cache (RMR_NPC_K: 1 or 2) of BVH scenes.
 std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
-                       const std::vector<char>* live = nullptr, bool split = true);
+                       const std::vector<char>* live = nullptr, bool split = true, int npc_k = 2);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);

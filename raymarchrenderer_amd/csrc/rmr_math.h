@@ -17,6 +17,7 @@ typedef __hip_internal::uint32_t uint32_t;
 typedef __hip_internal::int64_t int64_t;
 typedef __hip_internal::uint64_t uint64_t;
 typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
 #endif
 
 namespace rmr {

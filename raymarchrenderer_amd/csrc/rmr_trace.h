@@ -848,6 +848,97 @@ RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int k
     return d;
 }
 
+// map_bvh_npc through the candidate grid (P.grid, built on the host: rmr_api.cpp build_grid). A cell
+// C lists every small primitive whose distance lower bound over C is <= U(C) + margin, U(C) = the
+// smallest distance upper bound over C of any primitive (large ones included), margin >= twice the
+// float evaluation error; so at any point of C every unlisted primitive's float distance is strictly
+// above the exact fold's minimum, and the fold's closed form over (large primitives, listed ones,
+// the seed) is the full fold's (map_bvh). Cells are inflated past the rounding of the cell index.
+// Each lane evaluates its own cell's list (per-lane loads, as many passes as the longest list of the
+// batch) instead of the wave's union of BVH nodes; the approximate fold, the uniqueness test and the
+// exact fallback are map_bvh_npc's, and the cache bound also takes the cell's bound of the unlisted
+// primitives. Lanes outside the grid (or in a cell without a list) take map_bvh_npc.
+RMR_D void npc_insert(float a, int k, float& u1, float& u2, float& u3, int& k1, int& k2) {
+    const bool lt1 = a < u1, lt2 = a < u2;
+    u3 = __builtin_amdgcn_fmed3f(u2, a, u3);
+    u2 = __builtin_amdgcn_fmed3f(u1, a, u2);
+    k2 = lt1 ? k1 : (lt2 ? k : k2);
+    k1 = lt1 ? k : k1;
+    u1 = fminf(u1, a);
+}
+// approximate distance of leaf-order primitive k (per-lane index; am_prim's value: a sphere is the
+// box of half-extent 0 minus its radius, as prim_dist_at)
+RMR_D float am_prim_at(const float4* q, V3 p) {
+    const float4 a = q[0], b = q[1];   // c.xyz r.x | r.yz type|index<<8 mat_id
+    const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
+    const V3 h = box ? v3(a.w, b.x, b.y) : v3s(0.0f);
+    const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - h;
+    const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
+    const V3 o = vmax0(qq);
+    return (k0 + __builtin_amdgcn_sqrtf(dot(o, o))) - (box ? 0.0f : a.w);
+}
+RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+    const float fx = floorf((p.x - P.grid_lo[0]) * P.grid_inv);
+    const float fy = floorf((p.y - P.grid_lo[1]) * P.grid_inv);
+    const float fz = floorf((p.z - P.grid_lo[2]) * P.grid_inv);
+    bool in = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.grid_dim[0] && fy < (float)P.grid_dim[1] &&
+              fz < (float)P.grid_dim[2];   // NaN: false
+    uint2 cell = make_uint2(0u, 0u);
+    if (in) {
+        cell = P.grid[((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx];
+        in = (cell.x >> 24) != 255u;
+    }
+    V2 d = v2(P.max_dist, -1.0f);
+    if (__ballot(!in)) {
+        if (!in) d = map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
+    }
+    if (!__ballot(in)) return d;
+    bool uniq = false;
+    if (in) {
+        const float R2 = P.am_r2;
+        float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff();
+        int k1 = -1, k2 = -1;
+        if (ks >= 0) {
+            u1 = ds;
+            k1 = ks;
+        }
+        CDPrim* pr = (CDPrim*)P.dprims;
+        for (int k = 0; k < P.grid_n_large; k++) {   // wave-uniform: scalar loads
+            const int type = pr[k].type & 0xff;
+            const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
+            const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
+            if (k == ks) continue;
+            npc_insert(am_prim(type, p, c, r), k, u1, u2, u3, k1, k2);
+        }
+        const uint32_t n = cell.x >> 24, off = cell.x & 0xffffffu;
+        for (uint32_t i = 0; i < n; i++) {
+            const int k = (int)P.grid_list[off + i];
+            if (k == ks) continue;
+            npc_insert(am_prim_at((const float4*)(P.dprims + k), p), k, u1, u2, u3, k1, k2);
+        }
+        RMR_COUNT(P.counters, active_lanes(), 12, 1);   // (the count build prices a listed primitive as a sphere)
+        const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
+        const bool alone = (u2 == __builtin_inff()) && (u1 < __builtin_inff());
+        uniq = (alone || u2 - u1 > margin) && k1 >= 0;
+        if (uniq) {
+            float mid;
+            int j;
+            const float dw = (k1 == ks) ? ds : prim_dist(P, k1, p, mid, j);
+            if (k1 == ks) mid = ms;
+            opu(d, dw, mid);
+            kw = (dw > P.max_dist) ? -1 : k1;
+            const float v = (RMR_NPC_K >= 2 && k2 >= 0) ? u3 : u2;
+            const float vlb = v - fmaf(fabsf(v) + R2, 0x1p-20f, 0x1p-39f);
+            kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
+            sb = fminf(vlb, __uint_as_float(cell.y));
+        }
+    }
+    if (__ballot(in && !uniq)) {
+        if (in && !uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);
+    }
+    return d;
+}
+
 // map_bvh_npc with a per-lane traversal: every lane walks the pre-order node list with its own
 // culling decisions (the same predicate as the wave-uniform walk, !(lb2 > t^2) with t from the
 // lane's own running minimum), one node test or one primitive per loop pass, so a pass costs one
@@ -955,6 +1046,7 @@ struct TableMap {
     }
     static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
         if (RMR_NPC_LANE && RMR_NPC_APPROX) return map_bvh_npc_lane(P, p, kw, kw2, sb, ks, js, ds, ms);
+        if (RMR_NPC_APPROX && P.grid) return map_grid_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
         return map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
 };

@@ -325,6 +325,52 @@ def test_culling_switches_bitexact(renderer, scene, bounces, spp):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scene,W,H", [("cornell5.scene", 1920, 1080), ("csg256.scene", 960, 540)])
+def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
+    """The same property at production frame sizes (rare events — NaN directions, near ties, cache
+    bounds at grazing angles — show up only over millions of paths): every per-sample radiance of a
+    2-spp frame is bitwise equal with the work-skipping paths on and off (tools/full_frame_sweep.sh
+    runs the other scene families)."""
+    _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
+    times = time_schedule(2, frame=7)
+    out = {}
+    renderer.set_jit(1)
+    try:
+        for flags in (abi.CULL_ALL, 0):
+            renderer.set_culling(flags)
+            renderer.reload()
+            out[flags] = renderer.trace_samples(times, (0, 0, W, H))
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+        renderer.set_jit(2)
+    a, b = out[abi.CULL_ALL], out[0]
+    same = (a.view(np.uint32) == b.view(np.uint32)).all(-1) | (np.isnan(a).any(-1) & np.isnan(b).any(-1))
+    assert same.all(), "%d of %d samples differ" % ((~same).sum(), same.size)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["csg256.scene", "csg64.scene"])
+def test_candidate_grid_full_frame_bitexact(renderer, monkeypatch, scene):
+    """The nearest-primitive cache's full map() through the candidate grid (rmr_trace.h map_grid_npc,
+    the default for BVH scenes) against the same cache over the BVH traversal (RMR_GRID=0, read at
+    scene load): every sample of a 960x540 2-spp frame bitwise equal."""
+    W, H = 960, 540
+    out = {}
+    renderer.set_jit(1)
+    try:
+        for grid in ("1", "0"):
+            monkeypatch.setenv("RMR_GRID", grid)
+            _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
+            out[grid] = renderer.trace_samples(time_schedule(2, frame=9), (0, 0, W, H))
+    finally:
+        monkeypatch.delenv("RMR_GRID")
+        renderer.set_jit(2)
+    a, b = out["1"], out["0"]
+    same = (a.view(np.uint32) == b.view(np.uint32)).all(-1) | (np.isnan(a).any(-1) & np.isnan(b).any(-1))
+    assert same.all(), "%d of %d samples differ" % ((~same).sum(), same.size)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene", ["cornell5.scene", "csg256.scene"])
 def test_scheduling_knobs_bitexact(scene):
     """Shading-batch size, refill threshold and persistent grid size (rmr_set_tuning) decide only

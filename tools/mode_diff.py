@@ -3,6 +3,7 @@ specialisation time (e.g. RMR_SMALL_NPC 0 2): renders per-sample planes of a fra
 the differing samples, and runs the CPU oracle on the first few to say which setting is exact.
 
     python tools/mode_diff.py RMR_SMALL_NPC 0 2 [--scene scenes/cornell5.scene] [--spp 4] [--bounces 4]
+    python tools/mode_diff.py culling 7 0 --scene scenes/csg256.scene    (rmr_set_culling flags)
 """
 import argparse
 import os
@@ -18,7 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("var")
 ap.add_argument("a")
 ap.add_argument("b")
-ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "cornell5.scene"))
+ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "cornell5.scene"), help="scene file, or 'builtin'")
 ap.add_argument("--variant", default="rm1")
 ap.add_argument("--spp", type=int, default=4)
 ap.add_argument("--bounces", type=int, default=4)
@@ -35,8 +36,14 @@ r = Renderer(0, W, H)
 r.set_jit(1)
 planes = {}
 for v in (a.a, a.b):
-    os.environ[a.var] = v
-    r.load_scene(a.scene, a.variant)
+    if a.var == "culling":   # rmr_set_culling flags instead of an environment switch
+        r.set_culling(int(v))
+    else:
+        os.environ[a.var] = v
+    if a.scene == "builtin":
+        r.load_builtin(a.variant)
+    else:
+        r.load_scene(a.scene, a.variant)
     r.set_params(prm)
     r.set_view(view)
     r.reload()
@@ -46,7 +53,8 @@ A, B = planes[a.a], planes[a.b]
 diff = np.any(A.view(np.uint32) != B.view(np.uint32), axis=-1) & ~(np.isnan(A).any(-1) & np.isnan(B).any(-1))
 ks, ys, xs = np.nonzero(diff)
 print("differing samples: %d of %d" % (len(ks), diff.size), flush=True)
-orc = oracle.Oracle(scene_compile.load_scene_file(a.scene, a.variant), prm, view, W, H)
+tables = scene_compile.compile_scene({}, a.variant) if a.scene == "builtin" else scene_compile.load_scene_file(a.scene, a.variant)
+orc = oracle.Oracle(tables, prm, view, W, H)
 for i in range(min(a.show, len(ks))):
     k, y, x = int(ks[i]), int(ys[i]), int(xs[i])
     cpu = orc.trace_samples(times, (x, y, x + 1, y + 1))[k, 0, 0]
