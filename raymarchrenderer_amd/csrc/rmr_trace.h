@@ -1797,6 +1797,46 @@ RMR_D void shade(const KParams& P, Lane& L) {
     }
 }
 
+// Lane state that only shading, refills and the end of a trace read (RM1 throughput / RM3 power and
+// hero wavelength, RNG chain, unit, channel, bounce count): parked in LDS, one word per lane per
+// field (conflict-free), while the nearest-primitive cache's inner march loop runs.
+#ifndef RMR_NPC_STASH
+#define RMR_NPC_STASH 1
+#endif
+constexpr int kColdWords = 9;
+template <int VAR>
+RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
+    s[0][t] = __uint_as_float(L.unit);
+    s[1][t] = L.gxt;
+    s[2][t] = L.gyt;
+    s[3][t] = L.rc;
+    if constexpr (VAR == RMR_VARIANT_RM3) {
+        s[4][t] = L.power;
+        s[5][t] = __uint_as_float(L.wl);
+    } else {
+        s[4][t] = L.color.x;
+        s[5][t] = L.color.y;
+        s[6][t] = L.color.z;
+    }
+    s[7][t] = __int_as_float(L.chan);
+    s[8][t] = __int_as_float(L.bounces);
+}
+template <int VAR>
+RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
+    L.unit = __float_as_uint(s[0][t]);
+    L.gxt = s[1][t];
+    L.gyt = s[2][t];
+    L.rc = s[3][t];
+    if constexpr (VAR == RMR_VARIANT_RM3) {
+        L.power = s[4][t];
+        L.wl = __float_as_uint(s[5][t]);
+    } else {
+        L.color = v3(s[4][t], s[5][t], s[6][t]);
+    }
+    L.chan = __float_as_int(s[7][t]);
+    L.bounces = __float_as_int(s[8][t]);
+}
+
 RMR_D bool is_active(int ph) { return ph == PH_MARCH || ph == PH_NORMAL || ph == PH_SHADOW; }
 RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_NEE; }
 
@@ -1863,6 +1903,9 @@ RMR_D void trace_main(const KParams& P) {
 #define RMR_STAMP(v)
 #endif
     __shared__ ChunkRay s_ray[4][CHUNK];   // per wave (256-thread blocks = 4 waves)
+    // cache kernels: the lane's shading-only state during the inner march loop (cold_put / cold_get)
+    constexpr bool kStash = MAP::kCache && HO && RMR_NPC_STASH;
+    __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
 #if RMR_NPC_LDS
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
@@ -1932,6 +1975,15 @@ RMR_D void trace_main(const KParams& P) {
         const bool act = is_active(L.phase);
         const uint64_t amask = __ballot(act);
         if constexpr (MAP::kCache && HO) {   // HO kernels only: normalized directions, fixed bounce offsets
+            // the shading-only lane state waits in LDS during the inner march loop: its registers are
+            // then free for the map, where the compiler would otherwise spill the lane to scratch at
+            // every loop entry (C4: ~0.5 TB of scratch writes per launch)
+            if constexpr (kStash) {
+                if (amask) {
+                    cold_put<VAR>(s_cold, (int)threadIdx.x, L);
+                    __asm__ volatile("" ::: "memory");
+                }
+            }
             for (bool go = amask != 0; go;) {   // inner march loop (see the non-cache path)
                 const bool act1 = is_active(L.phase);
                 // nearest-primitive cache: one primitive where the bound holds; lanes where it does not
@@ -2021,6 +2073,12 @@ RMR_D void trace_main(const KParams& P) {
                 iters += dm ? 1 : 0;
                 const uint64_t sm = __ballot(is_shade(L.phase));
                 go = RMR_INNER_MARCH && __ballot(is_active(L.phase)) && __popcll(sm) < T;
+            }
+            if constexpr (kStash) {
+                if (amask) {
+                    __asm__ volatile("" ::: "memory");
+                    cold_get<VAR>(s_cold, (int)threadIdx.x, L);
+                }
             }
         } else if (MAP::kStepped && amask) {
             // stepped map() (the Mandelbulb one loop iteration per wave iteration): every active lane
