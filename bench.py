@@ -143,25 +143,30 @@ def cfg_name_of(cfg):
     return None
 
 
-GOLDEN_OF = {"c1": "img_rm1_sphere1_b1.npz", "c2": "img_rm1_cornell5_b4.npz"}
+# reference render per config (tests/golden/, llvmpipe): (file, scene it was rendered from). C4's is
+# csg256's generator cut to 64 primitives (the reference's codegen does not finish 256 on llvmpipe);
+# C5's is the animation's frame 0 (the sphere at y = 0 is the static Cornell-5 scene)
+GOLDEN_OF = {"c1": ("img_rm1_sphere1_b1.npz", "sphere1.scene"), "c2": ("img_rm1_cornell5_b4.npz", "cornell5.scene"),
+             "c3": ("img_rm1_mandelbulb_b2.npz", "mandelbulb.scene"), "c4": ("img_rm1_csg64_b4.npz", "csg64.scene"),
+             "c5": ("img_rm1_cornell5_b4.npz", "cornell5.scene")}
 
 
 def psnr_vs_reference(cfg_name, cfg, device):
     """PSNR of a converged GPU render against the reference GLSL's own converged render of the same
     scene (Mesa llvmpipe, tests/golden/, generated by oracle/glsl_ref/make_goldens.py) on the shared
-    small-seed schedule. Outside the timed region; None for configs without one."""
+    small-seed schedule. Outside the timed region."""
     import numpy as np
     from raymarchrenderer_amd import Renderer, abi, parity_schedule
-    name = GOLDEN_OF.get(cfg_name)
-    if not name:
+    if cfg_name not in GOLDEN_OF:
         return None
+    name, scene = GOLDEN_OF[cfg_name]
     g = np.load(os.path.join(ROOT, "tests", "golden", name))
     ref = g["conv"]
     H, W = ref.shape[:2]
     n = int(g["spp_conv"])
     r = Renderer(device, W, H)
     try:
-        r.load_scene(os.path.join(ROOT, "scenes", cfg["scene"]), "rm1")
+        r.load_scene(os.path.join(ROOT, "scenes", scene), "rm1")
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
         r.set_view(g["view"])
         r.render_spp(parity_schedule(n))
@@ -173,7 +178,7 @@ def psnr_vs_reference(cfg_name, cfg, device):
     psnr = 10 * np.log10(1.0 / max(np.mean((a - b) ** 2), 1e-30))
     rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(float(ref[..., :3].mean()), 1e-12)
     return {"psnr_db": round(float(psnr), 2), "mean_rel_diff": round(float(rel), 5),
-            "reference": "RayMarch.glsl on Mesa llvmpipe, %dx%d, %d spp (tests/golden/%s)" % (W, H, n, name),
+            "reference": "RayMarch.glsl on Mesa llvmpipe, %s, %dx%d, %d spp (tests/golden/%s)" % (scene, W, H, n, name),
             "gpu_spp": n}
 
 

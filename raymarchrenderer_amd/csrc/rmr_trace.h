@@ -639,7 +639,24 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
 // Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id ms;
 // ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
 // distance tightens the culling bound from the first node on.
-RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
+// Inlining of the cache's rarely taken full-map paths (register pressure of the cached kernel): 0 all
+// inline; 1 the exact traversal (near ties, NaN points) is a call; 2 also the BVH traversal of lanes
+// outside the candidate grid. Measured: calls are 3.1-3.4x slower on csg256 (the call convention
+// saves the caller's live registers to scratch around every call), so 0.
+#ifndef RMR_NPC_NOINLINE
+#define RMR_NPC_NOINLINE 0
+#endif
+#if RMR_NPC_NOINLINE >= 1
+#define RMR_NPC_EXACT_ATTR __device__ __noinline__
+#else
+#define RMR_NPC_EXACT_ATTR RMR_D
+#endif
+#if RMR_NPC_NOINLINE >= 2
+#define RMR_NPC_BVH_ATTR __device__ __noinline__
+#else
+#define RMR_NPC_BVH_ATTR RMR_D
+#endif
+RMR_NPC_EXACT_ATTR V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
                            bool count = true) {
     (void)count;
     typedef const __attribute__((address_space(4))) BvhNode CNode;
@@ -734,7 +751,7 @@ RMR_D float am_prim(int type, V3 p, V3 c, V3 r) {
 #ifndef RMR_NPC_HOIST
 #define RMR_NPC_HOIST 1
 #endif
-RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+RMR_NPC_BVH_ATTR V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
     if (!RMR_NPC_APPROX) return map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
@@ -1876,12 +1893,22 @@ constexpr int trace_waves() {
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
 #endif
+#ifndef RMR_WAVE_COUNT64
+#define RMR_WAVE_COUNT64 0
+#endif
+#if RMR_WAVE_COUNT64
+typedef uint64_t WCount;
+#else
+typedef uint32_t WCount;
+#endif
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
-    uint64_t maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, steps = 0;
+    // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
+    // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
+    WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, steps = 0;
     MBStep mbs;   // stepped map() state (MAP::kStepped)
     mbs.i = -1;
     bool maps_done = false;
@@ -2069,7 +2096,7 @@ RMR_D void trace_main(const KParams& P) {
                     else march_update<HO, true>(P, L, m);
                 }
                 const uint64_t dm = __ballot(done);
-                maps += (uint64_t)__popcll(dm);
+                maps += (WCount)__popcll(dm);
                 iters += dm ? 1 : 0;
                 const uint64_t sm = __ballot(is_shade(L.phase));
                 go = RMR_INNER_MARCH && __ballot(is_active(L.phase)) && __popcll(sm) < T;
@@ -2100,9 +2127,9 @@ RMR_D void trace_main(const KParams& P) {
                         maps_done = true;
                     }
                 }
-                maps += (uint64_t)__popcll(__ballot(maps_done));
+                maps += (WCount)__popcll(__ballot(maps_done));
                 maps_done = false;
-                steps += (uint64_t)__popcll(am);
+                steps += (WCount)__popcll(am);
                 iters++;
                 if (!RMR_INNER_MARCH) break;
                 const uint64_t sm = __ballot(is_shade(L.phase));
@@ -2122,7 +2149,7 @@ RMR_D void trace_main(const KParams& P) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO>(P, L, m);
                 }
-                maps += (uint64_t)__popcll(am);
+                maps += (WCount)__popcll(am);
                 iters++;
                 if (!RMR_INNER_MARCH) break;
                 const uint64_t sm = __ballot(is_shade(L.phase));
@@ -2135,7 +2162,7 @@ RMR_D void trace_main(const KParams& P) {
         const uint64_t amask2 = __ballot(is_active(L.phase));
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
-            shaded += (uint64_t)__popcll(smask);
+            shaded += (WCount)__popcll(smask);
             if (is_shade(L.phase)) shade<VAR, PROG, MATS>(P, L);
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
@@ -2147,15 +2174,23 @@ RMR_D void trace_main(const KParams& P) {
         cyc[2] += c3 - c2;
 #endif
         const uint64_t live = __ballot(L.phase != PH_IDLE);
-        if (live == 0 && exhausted) break;
+        const bool last = live == 0 && exhausted;
+        // (an inner loop adds at most 64 x its iterations to `maps`; a flush every 2^30 keeps every
+        // 32-bit counter far from wrapping between two checks)
+        if (last || ((maps | steps | shaded) >> 30) != 0) {
+            if (__lane_id() == 0) {
+                atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
+                atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
+                atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
+                if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
+                if (MAP::kStepped) atomicAdd(P.counters + 3, (unsigned long long)steps);   // lane-level estimator steps
+                atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
+            }
+            maps = iters = shades = fulls = shaded = steps = 0;
+        }
+        if (last) break;
     }
     if (__lane_id() == 0) {
-        atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
-        atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
-        atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
-        if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
-        if (MAP::kStepped) atomicAdd(P.counters + 3, (unsigned long long)steps);   // lane-level estimator steps
-        atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);

@@ -39,6 +39,10 @@ CASES = {
     # C3's Mandelbulb node in the reference path (oracle/glsl_ref/shader_build.py X1; the driver's own
     # transcendentals, so the distance estimate agrees to ~3e-5 and the images by PSNR)
     "rm1_mandelbulb_b2": (os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}, 40.0),
+    # C4's family: csg256's generator cut to 64 primitives (the reference's codegen compiles 64 on
+    # llvmpipe in ~100 s; 256 does not finish), through the BVH map, the nearest-primitive cache and the
+    # candidate grid
+    "rm1_csg64_b4": (os.path.join(SCENES, "csg64.scene"), "rm1", {"max_bounces": 4}, 40.0),
 }
 
 
