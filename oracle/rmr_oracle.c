@@ -84,6 +84,34 @@ static void mb_iter8(o_v3* z, float* dr, o_v3 p0, float r) {
     *dr = fmaf(8.0f * r7, *dr, 1.0f);
     *z = v_fma(o3(st * cp, sp * st, ct), r8, p0);
 }
+/* power 8 as complex powers (csrc/rmr_trace.h mb_iter8_poly, the same operations): (z.z + i sqrt(a))^8
+ * and (z.x + i z.y)^8 by two squarings each in a = x^2 + y^2, b = z^2; mb_iter8 near the z axis */
+static void mb_iter8_poly(o_v3* z, float* dr, o_v3 p0, float r) {
+    const float c = z->x * z->x, d = z->y * z->y, b = z->z * z->z;
+    const float a = c + d;
+    if (!(a >= 0x1p-30f)) {
+        mb_iter8(z, dr, p0, r);
+        return;
+    }
+    const float bma = b - a;
+    const float ab4 = (4.0f * a) * b;
+    const float re4 = fmaf(bma, bma, -ab4);
+    const float re8 = fmaf(re4, re4, -((4.0f * ab4) * (bma * bma)));
+    const float cmd = c - d;
+    const float re4p = fmaf(cmd, cmd, -((4.0f * c) * d));
+    const float im4p = ((4.0f * z->x) * z->y) * cmd;
+    const float re8p = fmaf(re4p, re4p, -(im4p * im4p));
+    const float im8p = (2.0f * re4p) * im4p;
+    const float a2 = a * a;
+    const float w = sqrtf(a) / (a2 * a2);
+    const float t = (((8.0f * z->z) * bma) * re4) * w;
+    const float r2 = r * r, r4 = r2 * r2, r7 = (r4 * r2) * r;
+    *dr = fmaf(8.0f * r7, *dr, 1.0f);
+    *z = v_add(o3(t * re8p, t * im8p, re8), p0);
+}
+#ifndef RMR_MB_POLY
+#define RMR_MB_POLY 1
+#endif
 /* map_mandelbulb — new node: power-N bulb, distance 0.5*log(r)*r/dr */
 static float sd_mandelbulb(o_v3 p, o_v3 c, o_v3 prm) {
     o_v3 p0 = v_sub(p, c);
@@ -95,7 +123,8 @@ static float sd_mandelbulb(o_v3 p, o_v3 c, o_v3 prm) {
         r = v_length(z);
         if (r > bail) break;
         if (power == 8.0f) {
-            mb_iter8(&z, &dr, p0, r);
+            if (RMR_MB_POLY) mb_iter8_poly(&z, &dr, p0, r);
+            else mb_iter8(&z, &dr, p0, r);
             continue;
         }
         float theta = det_acos(z.z / r);

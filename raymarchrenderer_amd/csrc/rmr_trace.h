@@ -111,10 +111,11 @@ RMR_D void count_work(unsigned long long* cnt, uint64_t lanes, uint64_t flops_pe
     }
 }
 #define RMR_COUNT(cnt, lanes, f, t) count_work((cnt), (lanes), (f), (t))
-// Mandelbulb iteration: 27 flops + 10 transcendentals (trigonometric form), 59 flops + 2 square
-// roots (power 8, mb_iter8)
-#define RMR_COUNT_MB(cnt, lanes, power) \
-    ((power) == 8.0f ? count_work((cnt), (lanes), 59, 2, 59) : count_work((cnt), (lanes), 27, 10, 27))
+// Mandelbulb iteration (|z| included): 27 flops + 10 transcendentals (trigonometric form); power 8:
+// 51 flops + 2 square roots (mb_iter8_poly; divisions count as one flop), 59 + 2 (mb_iter8)
+#define RMR_COUNT_MB(cnt, lanes, power)                                                            \
+    ((power) == 8.0f ? (RMR_MB_POLY ? count_work((cnt), (lanes), 51, 2, 51) : count_work((cnt), (lanes), 59, 2, 59)) \
+                     : count_work((cnt), (lanes), 27, 10, 27))
 #else
 #define RMR_COUNT(cnt, lanes, f, t) ((void)0)
 #define RMR_COUNT_MB(cnt, lanes, power) ((void)0)
@@ -197,11 +198,46 @@ RMR_D void mb_iter8(V3& z, float& dr, V3 p0, float r) {
     dr = fmaf(8.0f * r7, dr, 1.0f);
     z = vfma(v3(st * cp, sp * st, ct), r8, p0);
 }
+// Power 8 as complex powers (the default): with b = z.z^2, c = z.x^2, d = z.y^2, a = c + d,
+// (z.z + i sqrt(a))^8 = r^8 (cos 8 theta + i sin 8 theta) and (z.x + i z.y)^8 = a^4 (cos 8 phi +
+// i sin 8 phi), each by two squarings of (re, im) written in a, b (c, d): z^8 = (t Re', t Im', Re)
+// with t = 8 z.z (b - a) Re4 sqrt(a) / a^4 — one correctly rounded square root and one division
+// per iteration instead of two of each. The same function as mb_iter8, rounded differently; near
+// the z axis (a < 2^-30, where a^4 would leave the normal range) the iteration is mb_iter8's.
+// (oracle/rmr_oracle.c states the identical operations.)
+#ifndef RMR_MB_POLY
+#define RMR_MB_POLY 1
+#endif
+RMR_D void mb_iter8_poly(V3& z, float& dr, V3 p0, float r) {
+    const float c = z.x * z.x, d = z.y * z.y, b = z.z * z.z;
+    const float a = c + d;
+    if (!(a >= 0x1p-30f)) {   // (NaN too)
+        mb_iter8(z, dr, p0, r);
+        return;
+    }
+    const float bma = b - a;
+    const float ab4 = (4.0f * a) * b;
+    const float re4 = fmaf(bma, bma, -ab4);                         // r^4 cos 4 theta
+    const float re8 = fmaf(re4, re4, -((4.0f * ab4) * (bma * bma)));  // r^8 cos 8 theta
+    const float cmd = c - d;
+    const float re4p = fmaf(cmd, cmd, -((4.0f * c) * d));            // a^2 cos 4 phi
+    const float im4p = ((4.0f * z.x) * z.y) * cmd;                     // a^2 sin 4 phi
+    const float re8p = fmaf(re4p, re4p, -(im4p * im4p));              // a^4 cos 8 phi
+    const float im8p = (2.0f * re4p) * im4p;                          // a^4 sin 8 phi
+    const float a2 = a * a;
+    const float w = sqrt_cr(a) / (a2 * a2);
+    const float t = (((8.0f * z.z) * bma) * re4) * w;                 // r^8 sin 8 theta / a^4
+    const float r2 = r * r, r4 = r2 * r2, r7 = (r4 * r2) * r;
+    dr = fmaf(8.0f * r7, dr, 1.0f);
+    z = v3(t * re8p, t * im8p, re8) + p0;
+}
+
 // One iteration of the distance estimator's loop body after the bailout test (r = |z| <= bail):
 // z <- z^power + p0 in spherical form, dr <- power r^(power-1) dr + 1.
 RMR_D void mb_iter(V3& z, float& dr, V3 p0, float power, float r) {
     if (power == 8.0f) {
-        mb_iter8(z, dr, p0, r);
+        if (RMR_MB_POLY) mb_iter8_poly(z, dr, p0, r);
+        else mb_iter8(z, dr, p0, r);
         return;
     }
     float theta = det_acos(z.z / r);
@@ -247,18 +283,26 @@ struct MBStep {
     int i;         // loop index; -1: no map() in progress
     V2 pre;        // opU fold of the primitives before the Mandelbulb
 };
+// RMR_MB_STEP_K loop iterations per wave pass (the per-pass begin / finish cost against the lanes'
+// different bailout counts)
+#ifndef RMR_MB_STEP_K
+#define RMR_MB_STEP_K 1
+#endif
 RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, float& r, unsigned long long* cnt) {
     (void)cnt;
     if (iters <= 0) {   // the loop does not run: r stays 0
         r = 0.0f;
         return true;
     }
-    r = length(s.z);
-    if (r > bail) return true;
-    RMR_COUNT_MB(cnt, active_lanes(), power);
-    mb_iter(s.z, s.dr, s.p0, power, r);
-    s.i++;
-    return s.i >= iters;
+    for (int k = 0; k < RMR_MB_STEP_K; k++) {
+        r = length(s.z);
+        if (r > bail) return true;
+        RMR_COUNT_MB(cnt, active_lanes(), power);
+        mb_iter(s.z, s.dr, s.p0, power, r);
+        s.i++;
+        if (s.i >= iters) return true;
+    }
+    return false;
 }
 
 // Register file of a generated function (vec3 vars[total_vars]); indices are wave-uniform.
