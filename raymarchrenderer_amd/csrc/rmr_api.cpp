@@ -78,7 +78,7 @@ struct rmr_ctx {
     uint2* d_grid = nullptr;
     uint16_t* d_grid_list = nullptr;
     bool grid_on = false;
-    float grid_lo[3] = {0, 0, 0}, grid_inv = 1.0f;
+    float grid_lo[3] = {0, 0, 0}, grid_inv = 1.0f, grid_sbox[6] = {0, 0, 0, 0, 0, 0};
     int grid_dim[3] = {0, 0, 0}, grid_n_large = 0;
     int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
     bool has_prog = true;  // RM1 scene has materials needing the generic node interpreter
@@ -463,8 +463,8 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
             lo[k] = std::min(lo[k], (double)dp[(size_t)i].c[k] - half(dp[(size_t)i], k));
             hi[k] = std::max(hi[k], (double)dp[(size_t)i].c[k] + half(dp[(size_t)i], k));
         }
-    // the region: the small primitives' box grown by pad x its largest extent on every side, clipped
-    // to the box of all primitives (large ones included) grown by one cell
+    // the region: the small primitives' box grown by pad x its largest extent on every side, its lower
+    // side clipped to the box of all primitives (large ones included) grown by one cell
     double target = 262144.0, pad = 0.5;
     if (const char* e = std::getenv("RMR_GRID_CELLS")) target = std::max(1.0, std::atof(e));
     if (const char* e = std::getenv("RMR_GRID_PAD")) pad = std::max(0.0, std::atof(e));
@@ -481,10 +481,7 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
         rhi[k] = hi[k] + pad * ext;
     }
     double cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
-    for (int k = 0; k < 3; k++) {
-        rlo[k] = std::max(rlo[k], alo[k] - cs);
-        rhi[k] = std::min(rhi[k], ahi[k] + cs);
-    }
+    for (int k = 0; k < 3; k++) rlo[k] = std::max(rlo[k], alo[k] - cs);   // (march points above the scene occur)
     cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
     for (int k = 0; k < 3; k++) cs = std::max(cs, (rhi[k] - rlo[k]) / 1024.0);
     if (!(cs > 0.0) || !std::isfinite(cs)) return RMR_OK;
@@ -596,7 +593,15 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
     int r;
     if ((r = dev_upload(c, &c->d_grid, cells.data(), cells.size()))) return r;
     if ((r = dev_upload(c, &c->d_grid_list, flat.data(), flat.size()))) return r;
-    for (int k = 0; k < 3; k++) { c->grid_lo[k] = flo[k]; c->grid_dim[k] = dim[k]; }
+    for (int k = 0; k < 3; k++) {
+        c->grid_lo[k] = flo[k];
+        c->grid_dim[k] = dim[k];
+        float l = (float)lo[k], h = (float)hi[k];   // the small primitives' box, rounded outward
+        if ((double)l > lo[k]) l = std::nextafter(l, -HUGE_VALF);
+        if ((double)h < hi[k]) h = std::nextafter(h, HUGE_VALF);
+        c->grid_sbox[k] = l;
+        c->grid_sbox[3 + k] = h;
+    }
     c->grid_inv = finv;
     c->grid_n_large = n_large;
     c->grid_on = true;
@@ -787,6 +792,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     if (c->grid_on && c->map_np == -2) {
         P.grid = c->d_grid; P.grid_list = c->d_grid_list; P.grid_inv = c->grid_inv; P.grid_n_large = c->grid_n_large;
         for (int k = 0; k < 3; k++) { P.grid_lo[k] = c->grid_lo[k]; P.grid_dim[k] = c->grid_dim[k]; }
+        for (int k = 0; k < 6; k++) P.grid_sbox[k] = c->grid_sbox[k];
     }
     P.n_prims = (int)s.prims.size();
     P.am_r2 = 2.0f * rmr::max_sphere_radius(s);

@@ -68,6 +68,7 @@ struct KParams {
     float grid_inv;             // 1 / cell size
     int32_t grid_dim[3];
     int32_t grid_n_large;
+    float grid_sbox[6];         // box of the small primitives (lo.xyz, hi.xyz), rounded outward
     float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)
     float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     float npc_eps0;             // nearest-primitive cache: 2^-17 E + 2^-60 (rmr_trace.h npc_eps)

@@ -939,6 +939,7 @@ RMR_D float am_prim_at(const float4* q, V3 p) {
     return (k0 + __builtin_amdgcn_sqrtf(dot(o, o))) - (box ? 0.0f : a.w);
 }
 RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+    const float R2 = P.am_r2;
     const float fx = floorf((p.x - P.grid_lo[0]) * P.grid_inv);
     const float fy = floorf((p.y - P.grid_lo[1]) * P.grid_inv);
     const float fz = floorf((p.z - P.grid_lo[2]) * P.grid_inv);
@@ -949,29 +950,68 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         cell = P.grid[((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx];
         in = (cell.x >> 24) != 255u;
     }
-    V2 d = v2(P.max_dist, -1.0f);
-    if (__ballot(!in)) {
-        if (!in) d = map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
+    // the seed and the large primitives, every lane (approximate fold, am_*)
+    float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff();
+    int k1 = -1, k2 = -1;
+    if (ks >= 0) {
+        u1 = ds;
+        k1 = ks;
     }
-    if (!__ballot(in)) return d;
+    CDPrim* pr = (CDPrim*)P.dprims;
+    for (int k = 0; k < P.grid_n_large; k++) {   // wave-uniform: scalar loads
+        const int type = pr[k].type & 0xff;
+        const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
+        const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
+        if (k == ks) continue;
+        npc_insert(am_prim(type, p, c, r), k, u1, u2, u3, k1, k2);
+    }
+    // lower bound of every unlisted primitive's float distance: the cell's, or outside the grid the
+    // distance to the small primitives' box (each small primitive lies in it; its float distance is
+    // >= the Euclidean distance to its own box minus npc_eps) — there a lane whose seed / large minimum
+    // is below it needs no list at all ("far": the distant ground plane, the sky)
+    float bout = __uint_as_float(cell.y);
+    bool use = in;
+    if (!in) {
+        const V3 q = vmax0(vmax(v3(P.grid_sbox[0], P.grid_sbox[1], P.grid_sbox[2]) - p,
+                                p - v3(P.grid_sbox[3], P.grid_sbox[4], P.grid_sbox[5])));
+        bout = fmaf(__builtin_amdgcn_sqrtf(dot(q, q)), 1.0f - 0x1p-20f, -npc_eps(P, p));
+        const float sum = p.x + p.y + p.z;
+        use = (sum == sum) && bout > u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f);
+    }
+    V2 d = v2(P.max_dist, -1.0f);
+#ifdef RMR_GRID_STATS
+    {
+        const uint64_t outm = __ballot(!use), farm = __ballot(use && !in);
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
+            atomicAdd(P.counters + 9, (unsigned long long)__popcll(outm));   // lanes taking the BVH
+            atomicAdd(P.counters + 10, outm ? 1ull : 0ull);                  // batches with a BVH part
+            atomicAdd(P.counters + 12, (unsigned long long)__popcll(farm));  // lanes outside, no list needed
+        }
+    }
+#endif
+    if (__ballot(!use)) {
+        if (!use) d = map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
+    }
+    if (!__ballot(use)) return d;
     bool uniq = false;
-    if (in) {
-        const float R2 = P.am_r2;
-        float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff();
-        int k1 = -1, k2 = -1;
-        if (ks >= 0) {
-            u1 = ds;
-            k1 = ks;
+    if (use) {
+        const uint32_t n = in ? cell.x >> 24 : 0u, off = cell.x & 0xffffffu;
+#ifdef RMR_GRID_STATS   // diagnostics (RMR_JIT_OPTS=-DRMR_GRID_STATS, tools/grid_stats.py)
+        {
+            uint32_t mx = n, sm = n;
+            for (int o = 32; o > 0; o >>= 1) {
+                mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+                sm += (uint32_t)__shfl_xor((int)sm, o);
+            }
+            const uint64_t lanes = __ballot(1);
+            if (__lane_id() == __ffsll((unsigned long long)lanes) - 1) {
+                atomicAdd(P.counters + 4, 1ull);                                 // grid batches
+                atomicAdd(P.counters + 5, (unsigned long long)mx);               // longest list per batch
+                atomicAdd(P.counters + 6, (unsigned long long)sm);               // listed primitives (lanes)
+                atomicAdd(P.counters + 7, (unsigned long long)__popcll(lanes));  // lanes in grid batches
+            }
         }
-        CDPrim* pr = (CDPrim*)P.dprims;
-        for (int k = 0; k < P.grid_n_large; k++) {   // wave-uniform: scalar loads
-            const int type = pr[k].type & 0xff;
-            const V3 c = v3(pr[k].c[0], pr[k].c[1], pr[k].c[2]);
-            const V3 r = v3(pr[k].r[0], pr[k].r[1], pr[k].r[2]);
-            if (k == ks) continue;
-            npc_insert(am_prim(type, p, c, r), k, u1, u2, u3, k1, k2);
-        }
-        const uint32_t n = cell.x >> 24, off = cell.x & 0xffffffu;
+#endif
         for (uint32_t i = 0; i < n; i++) {
             const int k = (int)P.grid_list[off + i];
             if (k == ks) continue;
@@ -991,11 +1031,11 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
             const float v = (RMR_NPC_K >= 2 && k2 >= 0) ? u3 : u2;
             const float vlb = v - fmaf(fabsf(v) + R2, 0x1p-20f, 0x1p-39f);
             kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
-            sb = fminf(vlb, __uint_as_float(cell.y));
+            sb = fminf(vlb, bout);
         }
     }
-    if (__ballot(in && !uniq)) {
-        if (in && !uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);
+    if (__ballot(use && !uniq)) {
+        if (use && !uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);
     }
     return d;
 }
