@@ -651,8 +651,10 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 // Where the cached primitives are read from: the leaf-ordered DPrim table itself (global, per-lane
 // vector loads through the L1) or, with RMR_NPC_LDS, a copy of it staged in the workgroup's LDS at
 // kernel start (scenes of <= RMR_NPC_LDS_MAX primitives).
+// (csg256 8 spp: 26.2 -> 25.6 ms with the table in LDS and 32-unit chunks, which keep the block's LDS
+// at 20 KiB = 8 blocks per CU; with 64-unit chunks the LDS cost two waves per SIMD: slower)
 #ifndef RMR_NPC_LDS
-#define RMR_NPC_LDS 0
+#define RMR_NPC_LDS 1
 #endif
 #ifndef RMR_NPC_LDS_MAX
 #define RMR_NPC_LDS_MAX 256
@@ -1904,7 +1906,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
 #ifndef RMR_NPC_STASH
 #define RMR_NPC_STASH 1
 #endif
-constexpr int kColdWords = 9;
+constexpr int kColdWords = 8;
 template <int VAR>
 RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
     s[0][t] = __uint_as_float(L.unit);
@@ -1919,8 +1921,7 @@ RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
         s[5][t] = L.color.y;
         s[6][t] = L.color.z;
     }
-    s[7][t] = __int_as_float(L.chan);
-    s[8][t] = __int_as_float(L.bounces);
+    s[7][t] = __int_as_float((L.chan + 1) | (L.bounces << 8));   // chan in [-1, 2], bounces >= 0
 }
 template <int VAR>
 RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
@@ -1934,8 +1935,9 @@ RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
     } else {
         L.color = v3(s[4][t], s[5][t], s[6][t]);
     }
-    L.chan = __float_as_int(s[7][t]);
-    L.bounces = __float_as_int(s[8][t]);
+    const int cb = __float_as_int(s[7][t]);
+    L.chan = (cb & 0xff) - 1;
+    L.bounces = cb >> 8;
 }
 
 RMR_D bool is_active(int ph) { return ph == PH_MARCH || ph == PH_NORMAL || ph == PH_SHADOW; }
@@ -1972,7 +1974,7 @@ constexpr int trace_waves() {
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
 #ifndef RMR_CHUNK_CACHE
-#define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (csg256: +3.7% over 128)
+#define RMR_CHUNK_CACHE 32   // the same for the nearest-primitive cache kernels (LDS budget, RMR_NPC_LDS)
 #endif
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
@@ -2141,6 +2143,9 @@ RMR_D void trace_main(const KParams& P) {
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
                     pfin = sum == sum;
                     ok = pfin && (L.cs - delta - npc_eps(P, p) > Fm);
+#ifdef RMR_NPC_ALWAYS_FULL   // experiment: every map() through the full path (the candidate grid)
+                    ok = false;
+#endif
                 }
                 const uint64_t okm = __ballot(act1 && ok);
                 const uint64_t fm = __ballot(act1 && !ok);
