@@ -286,7 +286,7 @@ struct MBStep {
 // RMR_MB_STEP_K loop iterations per wave pass (the per-pass begin / finish cost against the lanes'
 // different bailout counts)
 #ifndef RMR_MB_STEP_K
-#define RMR_MB_STEP_K 1
+#define RMR_MB_STEP_K 2   // (C3 16 spp with mb_iter8_poly: K 1 / 2 / 3 -> 17.0 / 14.6 / 14.6 ms; whole map 14.2)
 #endif
 RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, float& r, unsigned long long* cnt) {
     (void)cnt;
