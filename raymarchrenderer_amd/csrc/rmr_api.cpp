@@ -346,7 +346,8 @@ int ensure_jit(rmr_ctx* c) {
     const bool split = c->sched == RMR_SCHED_SPLIT && rmr::jit_split_applies(c->scene, c->has_prog, c->cull);
     // one cached primitive when the cache's full map() runs through the candidate grid (csg256: 21.5 ->
     // 17.4 ms per 4 spp against two); two with the BVH full map
-    const int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
+    int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
+    if (const char* e = std::getenv("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
     const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, split, npc_k);
     std::vector<char> code;
     std::string key, log;
