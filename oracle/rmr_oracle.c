@@ -236,11 +236,25 @@ static o_v3 o_normal(lane* L, o_v3 p) {
 }
 
 /* randHemisphere(s1, s2, normal), RM1:270-304 */
+/* RMR_HEMI_ALGEBRAIC (default, csrc/rmr_trace.h hemisphere): cos(acos(u)) = u and
+ * sin(acos(u)) = sqrt(1 - u^2) >= 0 taken algebraically instead of through det_acos / det_sin / det_cos:
+ * the same direction, rounded differently (pinned by the distribution and PSNR tests) */
+#ifndef RMR_HEMI_ALGEBRAIC
+#define RMR_HEMI_ALGEBRAIC 1
+#endif
 static o_v3 o_hemisphere(lane* L, o_v2 s1, o_v2 s2, o_v3 n) {
     float theta = 6.28318548202514648438f * o_rand(L, s1); /* 2 * 3.141592653 */
-    float phi = det_acos(2.0f * o_rand(L, s2) - 1.0f);
-    float sp = det_sin(phi);
-    o_v3 b = v_normalize(o3(sp * det_cos(theta), det_cos(phi), sp * det_sin(theta)));
+    float sp, cp;
+    if (RMR_HEMI_ALGEBRAIC) {
+        const float u = 2.0f * o_rand(L, s2) - 1.0f;
+        cp = u;
+        sp = sqrtf(fmaxf(fmaf(-u, u, 1.0f), 0.0f));
+    } else {
+        float phi = det_acos(2.0f * o_rand(L, s2) - 1.0f);
+        sp = det_sin(phi);
+        cp = det_cos(phi);
+    }
+    o_v3 b = v_normalize(o3(sp * det_cos(theta), cp, sp * det_sin(theta)));
     if (!v_is_zero(n)) {
         if (b.z < 0.0f) b = v_neg(b);
         o_v3 lx;

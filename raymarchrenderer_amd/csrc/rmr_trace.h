@@ -135,12 +135,23 @@ RMR_D float rand_step(float gxt, float gyt, float& rc, V2 co) {
 }
 RMR_D float lrand(Lane& L, V2 co) { return rand_step(L.gxt, L.gyt, L.rc, co); }
 
-// randHemisphere, RM1:270-304
+// randHemisphere, RM1:270-304. RMR_HEMI_ALGEBRAIC (default; oracle/rmr_oracle.c o_hemisphere the
+// same): cos(acos(u)) = u and sin(acos(u)) = sqrt(1 - u^2) >= 0 algebraically instead of det_acos and
+// one det_sincos — the same direction, rounded differently (distribution and PSNR tests pin it)
+#ifndef RMR_HEMI_ALGEBRAIC
+#define RMR_HEMI_ALGEBRAIC 1
+#endif
 RMR_D V3 hemisphere(Lane& L, V2 s1, V2 s2, V3 n) {
     float theta = 6.28318548202514648438f * lrand(L, s1);
-    float phi = det_acos(2.0f * lrand(L, s2) - 1.0f);
     float sp, cp, st, ct;
-    det_sincos(phi, sp, cp);
+    if (RMR_HEMI_ALGEBRAIC) {
+        const float u = 2.0f * lrand(L, s2) - 1.0f;
+        cp = u;
+        sp = sqrt_cr(fmaxf(fmaf(-u, u, 1.0f), 0.0f));
+    } else {
+        const float phi = det_acos(2.0f * lrand(L, s2) - 1.0f);
+        det_sincos(phi, sp, cp);
+    }
     det_sincos(theta, st, ct);
     V3 b = normalize(v3(sp * ct, cp, sp * st));
     if (!is_zero(n)) {
