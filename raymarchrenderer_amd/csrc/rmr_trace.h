@@ -951,7 +951,9 @@ RMR_D float am_prim_at(const float4* q, V3 p) {
     const V3 o = vmax0(qq);
     return (k0 + __builtin_amdgcn_sqrtf(dot(o, o))) - (box ? 0.0f : a.w);
 }
-RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+// dtab: the leaf-ordered primitive table as float4 pairs (the LDS copy of trace_main when it has one)
+RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
+                      const float4* dtab) {
     const float R2 = P.am_r2;
     const float fx = floorf((p.x - P.grid_lo[0]) * P.grid_inv);
     const float fy = floorf((p.y - P.grid_lo[1]) * P.grid_inv);
@@ -1028,7 +1030,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         for (uint32_t i = 0; i < n; i++) {
             const int k = (int)P.grid_list[off + i];
             if (k == ks) continue;
-            npc_insert(am_prim_at((const float4*)(P.dprims + k), p), k, u1, u2, u3, k1, k2);
+            npc_insert(am_prim_at(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
         }
         RMR_COUNT(P.counters, active_lanes(), 12, 1);   // (the count build prices a listed primitive as a sphere)
         const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
@@ -1037,7 +1039,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         if (uniq) {
             float mid;
             int j;
-            const float dw = (k1 == ks) ? ds : prim_dist(P, k1, p, mid, j);
+            const float dw = (k1 == ks) ? ds : prim_dist_at(dtab + 2 * k1, p, mid, j);
             if (k1 == ks) mid = ms;
             opu(d, dw, mid);
             kw = (dw > P.max_dist) ? -1 : k1;
@@ -1158,9 +1160,10 @@ struct TableMap {
         else if constexpr (NP == -2 || NP == -3) return map_bvh(P, p);
         else return map_general(P, p);
     }
-    static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
+    static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
+                         const float4* dtab) {
         if (RMR_NPC_LANE && RMR_NPC_APPROX) return map_bvh_npc_lane(P, p, kw, kw2, sb, ks, js, ds, ms);
-        if (RMR_NPC_APPROX && P.grid) return map_grid_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
+        if (RMR_NPC_APPROX && P.grid) return map_grid_npc(P, p, kw, kw2, sb, ks, js, ds, ms, dtab);
         return map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
 };
@@ -2039,8 +2042,10 @@ RMR_D void trace_main(const KParams& P) {
         __syncthreads();
     }
 #define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_at(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
+#define RMR_DTAB (dp_lds ? (const float4*)s_dp : (const float4*)P.dprims)
 #else
 #define RMR_PRIM_DIST(k, p, mid, j) prim_dist(P, k, p, mid, j)
+#define RMR_DTAB ((const float4*)P.dprims)
 #endif
     const int wv = (threadIdx.x >> 6) & 3;
     uint32_t chunk_base = 0;
@@ -2169,7 +2174,7 @@ RMR_D void trace_main(const KParams& P) {
                         float s2;
                         // seeded with the cached primitive only at a finite point: prim_dist's box form
                         // of a sphere drops a NaN coordinate (fmaxf / fminf) where sd_sphere keeps it
-                        m = MAP::full(P, p, kw, kw2, s2, (pfin && F == F) ? L.cw : -1, jw, F, mid);
+                        m = MAP::full(P, p, kw, kw2, s2, (pfin && F == F) ? L.cw : -1, jw, F, mid, RMR_DTAB);
                         L.cw = kw >= 0 ? kw : 0;
                         L.cw2 = kw >= 0 ? kw2 : 0;
                         // |s2| 2^-20: the rounding of the check's own subtractions
