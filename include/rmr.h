@@ -186,6 +186,16 @@ int rmr_display_device(rmr_ctx* ctx, float centre_x, float centre_y, float zoom,
                        float max_x, float max_y, int screen_w, int screen_h, void* rgba8_dev);
 /* The 256 sRGB decision points rmr_display uses: out[k] = the smallest float c with byte(c) >= k. */
 int rmr_srgb_thresholds(float out[256]);
+/* Test hook, no GPU needed: the candidate grid a context builds for a BVH scene's nearest-primitive
+ * cache (rmr_trace.h map_grid_npc). prims: n rows of 8 floats in leaf order (c.xyz, r.xyz, type
+ * RMR_PRIM_SPHERE / RMR_PRIM_BOX as a float value, mat_id); rows [0, n_large) are evaluated everywhere
+ * (large primitives), the rest are gridded. E = max |c|_inf + |r|_inf over the scene. target / pad:
+ * cell count / region growth (<= 0: the context's defaults). Out: idims = (dim.xyz, list length,
+ * built 0/1); geom = (lo.xyz, 1 / cell size, small-primitive box lo.xyz hi.xyz, eps, margin); cells:
+ * 2 words per cell (offset | count << 24, bound bits); list: leaf indices. Returns RMR_E_INVALID with
+ * idims filled when cells_cap (words) or list_cap is too small. */
+int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double target, double pad, int32_t idims[5],
+                       float geom[12], uint32_t* cells, size_t cells_cap, uint16_t* list, size_t list_cap);
 /* Per-scene kernel specialisation (the reference recompiles its shader per scene, Graphics::Reload):
  * the scene's map() is generated as HIP source with the primitives as literals and compiled by
  * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under

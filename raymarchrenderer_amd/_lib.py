@@ -22,7 +22,7 @@ EXPORTS = [
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats", "rmr_get_section_cycles", "rmr_get_counters", "rmr_set_culling", "rmr_set_schedule",
     "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_jit_compile_scene", "rmr_set_env_map",
     "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free", "rmr_display", "rmr_display_device",
-    "rmr_srgb_thresholds",
+    "rmr_srgb_thresholds", "rmr_candidate_grid",
 ]
 
 
@@ -103,6 +103,9 @@ def lib():
         "rmr_display": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
         "rmr_display_device": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
         "rmr_srgb_thresholds": (C.c_int, [fp]),
+        "rmr_candidate_grid": (C.c_int, [fp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                         C.POINTER(C.c_int32), fp, C.POINTER(C.c_uint32), C.c_size_t,
+                                         C.POINTER(C.c_uint16), C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

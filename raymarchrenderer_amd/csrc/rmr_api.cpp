@@ -20,6 +20,7 @@
 
 #include "../../include/rmr.h"
 #include "rmr_internal.h"
+#include "grid.hpp"
 #include "rmr_jit.hpp"
 #include "scene.hpp"
 
@@ -449,161 +450,22 @@ void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>
 // anywhere in the grid, so an unlisted primitive's float distance is strictly above the minimum's);
 // the cell's bound = the smallest lower bound of an unlisted one, minus that error bound. Exact
 // arithmetic in double; cells of more than 254 candidates keep the BVH (count 255).
-// Env (experiments): RMR_GRID=0 off, RMR_GRID_CELLS (target cell count), RMR_GRID_PAD (cells).
+// Env (experiments): RMR_GRID=0 off, RMR_GRID_CELLS (target cell count), RMR_GRID_PAD (region pad).
+// The construction is host code (grid.cpp, build_candidate_grid); this uploads it.
 int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, double E) {
     c->grid_on = false;
     if (const char* e = std::getenv("RMR_GRID")) if (std::atoi(e) == 0) return RMR_OK;
-    const int n = (int)dp.size();
-    if (n - n_large < 1 || n > 65535) return RMR_OK;
-    auto half = [&](const rmr::DPrim& q, int k) {
-        return (double)std::fabs((q.type & 0xff) == RMR_PRIM_SPHERE ? q.r[0] : q.r[k]);
-    };
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    for (int i = n_large; i < n; i++)
-        for (int k = 0; k < 3; k++) {
-            lo[k] = std::min(lo[k], (double)dp[(size_t)i].c[k] - half(dp[(size_t)i], k));
-            hi[k] = std::max(hi[k], (double)dp[(size_t)i].c[k] + half(dp[(size_t)i], k));
-        }
-    // the region: the small primitives' box grown by pad x its largest extent on every side, its lower
-    // side clipped to the box of all primitives (large ones included) grown by one cell
     double target = 262144.0, pad = 0.5;
     if (const char* e = std::getenv("RMR_GRID_CELLS")) target = std::max(1.0, std::atof(e));
     if (const char* e = std::getenv("RMR_GRID_PAD")) pad = std::max(0.0, std::atof(e));
-    double alo[3] = {1e300, 1e300, 1e300}, ahi[3] = {-1e300, -1e300, -1e300};
-    for (int i = 0; i < n; i++)
-        for (int k = 0; k < 3; k++) {
-            alo[k] = std::min(alo[k], (double)dp[(size_t)i].c[k] - half(dp[(size_t)i], k));
-            ahi[k] = std::max(ahi[k], (double)dp[(size_t)i].c[k] + half(dp[(size_t)i], k));
-        }
-    const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
-    double rlo[3], rhi[3];
-    for (int k = 0; k < 3; k++) {
-        rlo[k] = lo[k] - pad * ext;
-        rhi[k] = hi[k] + pad * ext;
-    }
-    double cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
-    for (int k = 0; k < 3; k++) rlo[k] = std::max(rlo[k], alo[k] - cs);   // (march points above the scene occur)
-    cs = std::cbrt(std::max(1e-30, (rhi[0] - rlo[0]) * (rhi[1] - rlo[1]) * (rhi[2] - rlo[2])) / target);
-    for (int k = 0; k < 3; k++) cs = std::max(cs, (rhi[k] - rlo[k]) / 1024.0);
-    if (!(cs > 0.0) || !std::isfinite(cs)) return RMR_OK;
-    int dim[3];
-    float flo[3];
-    double pmax = E;
-    for (int k = 0; k < 3; k++) {
-        flo[k] = (float)rlo[k];
-        dim[k] = std::max(1, (int)std::ceil((rhi[k] - (double)flo[k]) / cs));
-        pmax = std::max(pmax, std::max(std::fabs((double)flo[k]), std::fabs((double)flo[k] + dim[k] * cs)));
-    }
-    const float finv = (float)(1.0 / cs);
-    const double csf = 1.0 / (double)finv;   // the cell size the kernel's index arithmetic implies
-    const size_t ncell = (size_t)dim[0] * dim[1] * dim[2];
-    if (ncell > ((size_t)1 << 24)) return RMR_OK;
-    // float error bound of a box/sphere distance at |p|_inf <= pmax (rmr_trace.h npc_eps, 4x slack)
-    const double eps = std::ldexp(pmax + E, -17);
-    const double margin = 4.0 * eps;
-    const double infl = 1e-4 + std::ldexp(pmax, -16) + 4.0 * std::ldexp(csf, -20);   // cell index rounding
-    struct PB { double c[3], h[3], rad; bool box; };
-    std::vector<PB> pb((size_t)n);
-    for (int i = 0; i < n; i++) {
-        const rmr::DPrim& q = dp[(size_t)i];
-        PB b{};
-        b.box = (q.type & 0xff) == RMR_PRIM_BOX;
-        for (int k = 0; k < 3; k++) { b.c[k] = q.c[k]; b.h[k] = b.box ? (double)q.r[k] : 0.0; }
-        b.rad = b.box ? 0.0 : (double)q.r[0];
-        pb[(size_t)i] = b;
-    }
-    // distance bounds of primitive b over the cell [a0, a1]: lower (Euclidean distance to the box of
-    // half-extent |h| minus the radius; -min|h| - rad when they overlap) and upper (the largest corner value)
-    auto bounds = [&](const PB& b, const double* a0, const double* a1, double& dmin, double& dmax) {
-        double s2 = 0.0, f2 = 0.0, mh = 1e300;
-        bool overlap = true;
-        for (int k = 0; k < 3; k++) {
-            const double h = std::fabs(b.h[k]);
-            const double gap = std::max({a0[k] - (b.c[k] + h), (b.c[k] - h) - a1[k], 0.0});
-            if (gap > 0.0) overlap = false;
-            s2 += gap * gap;
-            mh = std::min(mh, h);
-        }
-        dmin = overlap ? (b.box ? -mh : -b.rad) : std::sqrt(s2) - b.rad;
-        dmax = -1e300;
-        for (int corner = 0; corner < 8; corner++) {
-            double qv[3], mq = -1e300, o2 = 0.0;
-            for (int k = 0; k < 3; k++) {
-                const double x = (corner >> k) & 1 ? a1[k] : a0[k];
-                qv[k] = std::fabs(x - b.c[k]) - b.h[k];
-                mq = std::max(mq, qv[k]);
-                o2 += std::max(qv[k], 0.0) * std::max(qv[k], 0.0);
-            }
-            (void)f2;
-            dmax = std::max(dmax, std::min(mq, 0.0) + std::sqrt(o2) - b.rad);
-        }
-    };
-    std::vector<std::vector<uint16_t>> lists(ncell);
-    std::vector<uint32_t> cnt(ncell);
-    std::vector<float> lout(ncell);
-    auto work = [&](int z0, int z1) {
-        std::vector<double> dmn((size_t)n), dmx((size_t)n);
-        for (int z = z0; z < z1; z++)
-            for (int y = 0; y < dim[1]; y++)
-                for (int x = 0; x < dim[0]; x++) {
-                    const int ii[3] = {x, y, z};
-                    double a0[3], a1[3];
-                    for (int k = 0; k < 3; k++) {
-                        a0[k] = (double)flo[k] + ii[k] * csf - infl;
-                        a1[k] = (double)flo[k] + (ii[k] + 1) * csf + infl;
-                    }
-                    double U = 1e300;
-                    for (int i = 0; i < n; i++) {
-                        bounds(pb[(size_t)i], a0, a1, dmn[(size_t)i], dmx[(size_t)i]);
-                        U = std::min(U, dmx[(size_t)i]);
-                    }
-                    const size_t ci = ((size_t)z * dim[1] + y) * dim[0] + x;
-                    double lo_out = 1e300;
-                    std::vector<uint16_t>& L = lists[ci];
-                    for (int i = n_large; i < n; i++) {
-                        if (dmn[(size_t)i] <= U + margin) L.push_back((uint16_t)i);
-                        else lo_out = std::min(lo_out, dmn[(size_t)i]);
-                    }
-                    if (L.size() > 254) { cnt[ci] = 255; L.clear(); }
-                    else cnt[ci] = (uint32_t)L.size();
-                    float lf = lo_out >= 1e300 ? HUGE_VALF : (float)(lo_out - eps);
-                    if ((double)lf > lo_out - eps) lf = std::nextafter(lf, -HUGE_VALF);
-                    lout[ci] = lf;
-                }
-    };
-    {
-        const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        const int per = (dim[2] + nt - 1) / nt;
-        for (int t = 0; t < nt; t++) {
-            const int z0 = t * per, z1 = std::min(dim[2], z0 + per);
-            if (z0 < z1) th.emplace_back(work, z0, z1);
-        }
-        for (auto& t : th) t.join();
-    }
-    std::vector<uint2> cells(ncell);
-    std::vector<uint16_t> flat;
-    for (size_t i = 0; i < ncell; i++) {
-        if (flat.size() + lists[i].size() >= ((size_t)1 << 24)) return RMR_OK;
-        cells[i].x = (uint32_t)flat.size() | (cnt[i] << 24);
-        uint32_t lb;
-        std::memcpy(&lb, &lout[i], 4);
-        cells[i].y = lb;
-        flat.insert(flat.end(), lists[i].begin(), lists[i].end());
-    }
+    rmr::CandidateGrid g;
+    if (!rmr::build_candidate_grid(dp, n_large, E, target, pad, g)) return RMR_OK;
     int r;
-    if ((r = dev_upload(c, &c->d_grid, cells.data(), cells.size()))) return r;
-    if ((r = dev_upload(c, &c->d_grid_list, flat.data(), flat.size()))) return r;
-    for (int k = 0; k < 3; k++) {
-        c->grid_lo[k] = flo[k];
-        c->grid_dim[k] = dim[k];
-        float l = (float)lo[k], h = (float)hi[k];   // the small primitives' box, rounded outward
-        if ((double)l > lo[k]) l = std::nextafter(l, -HUGE_VALF);
-        if ((double)h < hi[k]) h = std::nextafter(h, HUGE_VALF);
-        c->grid_sbox[k] = l;
-        c->grid_sbox[3 + k] = h;
-    }
-    c->grid_inv = finv;
+    if ((r = dev_upload(c, &c->d_grid, (const uint2*)g.cells.data(), g.cells.size() / 2))) return r;
+    if ((r = dev_upload(c, &c->d_grid_list, g.list.data(), g.list.size()))) return r;
+    for (int k = 0; k < 3; k++) { c->grid_lo[k] = g.lo[k]; c->grid_dim[k] = g.dim[k]; }
+    for (int k = 0; k < 6; k++) c->grid_sbox[k] = g.sbox[k];
+    c->grid_inv = g.inv;
     c->grid_n_large = n_large;
     c->grid_on = true;
     return RMR_OK;
@@ -1302,6 +1164,37 @@ int rmr_set_kernel(rmr_ctx* c, int kernel) {
 // for c in [0, 1] (srgb: 12.92 c below 0.0031308, else 1.055 c^(1/2.4) - 0.055), so byte(c) >= k
 // <=> srgb(c) >= (k - 1/2) / 255 <=> c >= linear((k - 1/2) / 255); out[k] is that bound rounded up to
 // a float (for a float c the comparison is then exact), out[0] = 0.
+int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double target, double pad, int32_t idims[5],
+                       float geom[12], uint32_t* cells, size_t cells_cap, uint16_t* list, size_t list_cap) {
+    if (!prims || n <= 0 || n_large < 0 || n_large > n || !idims || !geom) return RMR_E_INVALID;
+    std::vector<rmr::DPrim> dp((size_t)n);
+    for (int i = 0; i < n; i++) {
+        const float* r = prims + 8 * (size_t)i;
+        rmr::DPrim q{};
+        for (int k = 0; k < 3; k++) { q.c[k] = r[k]; q.r[k] = r[3 + k]; }
+        q.type = (int32_t)r[6] | (i << 8);
+        q.mat_id = r[7];
+        dp[(size_t)i] = q;
+    }
+    rmr::CandidateGrid g;
+    const bool built = rmr::build_candidate_grid(dp, n_large, E, target > 0.0 ? target : 262144.0,
+                                                 pad > 0.0 ? pad : 0.5, g);
+    for (int k = 0; k < 5; k++) idims[k] = 0;
+    for (int k = 0; k < 12; k++) geom[k] = 0.0f;
+    idims[4] = built ? 1 : 0;
+    if (!built) return RMR_OK;
+    for (int k = 0; k < 3; k++) { idims[k] = g.dim[k]; geom[k] = g.lo[k]; }
+    idims[3] = (int32_t)g.list.size();
+    geom[3] = g.inv;
+    for (int k = 0; k < 6; k++) geom[4 + k] = g.sbox[k];
+    geom[10] = (float)g.eps;
+    geom[11] = (float)g.margin;
+    if (!cells || !list || cells_cap < g.cells.size() || list_cap < g.list.size()) return RMR_E_INVALID;
+    std::memcpy(cells, g.cells.data(), g.cells.size() * sizeof(uint32_t));
+    std::memcpy(list, g.list.data(), g.list.size() * sizeof(uint16_t));
+    return RMR_OK;
+}
+
 int rmr_srgb_thresholds(float out[256]) {
     if (!out) return RMR_E_INVALID;
     out[0] = 0.0f;

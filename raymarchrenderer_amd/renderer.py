@@ -472,3 +472,30 @@ def srgb_thresholds():
     if rc != abi.RMR_OK:
         raise RMRError(rc, "rmr_srgb_thresholds")
     return out
+
+
+def candidate_grid(prims, n_large, E, target=0.0, pad=0.0):
+    """rmr_candidate_grid (test hook, no GPU): the nearest-primitive cache's candidate grid for
+    `prims` (n x 8 float32 rows in leaf order: c.xyz, r.xyz, type, mat_id; the first n_large
+    evaluated everywhere). Returns a dict with dim, lo, inv, sbox, eps, margin, cells (n_cells x 2
+    uint32) and list (uint16), or None when no grid applies."""
+    prims = np.ascontiguousarray(prims, np.float32)
+    n = prims.shape[0]
+    idims = (C.c_int32 * 5)()
+    geom = np.zeros(12, np.float32)
+    rc = lib().rmr_candidate_grid(_fp(prims), n, int(n_large), float(E), float(target), float(pad), idims, _fp(geom),
+                                  None, 0, None, 0)
+    if rc not in (abi.RMR_OK, -1):   # -1 RMR_E_INVALID: buffers not given yet (sizes returned)
+        raise RMRError(rc, "rmr_candidate_grid")
+    if not idims[4]:
+        return None
+    ncell = idims[0] * idims[1] * idims[2]
+    cells = np.zeros(2 * ncell, np.uint32)
+    lst = np.zeros(max(1, idims[3]), np.uint16)
+    rc = lib().rmr_candidate_grid(_fp(prims), n, int(n_large), float(E), float(target), float(pad), idims, _fp(geom),
+                                  cells.ctypes.data_as(C.POINTER(C.c_uint32)), cells.size,
+                                  lst.ctypes.data_as(C.POINTER(C.c_uint16)), lst.size)
+    if rc != abi.RMR_OK:
+        raise RMRError(rc, "rmr_candidate_grid")
+    return {"dim": (idims[0], idims[1], idims[2]), "lo": geom[0:3].copy(), "inv": geom[3], "sbox": geom[4:10].copy(),
+            "eps": float(geom[10]), "margin": float(geom[11]), "cells": cells.reshape(-1, 2), "list": lst[:idims[3]]}
