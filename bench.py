@@ -42,6 +42,9 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec (pixels×spp) at 1920×1080; PSNR vs GLSL reference"
 TILE = 32
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
+# measured on the box by tools/probes/fma_peak.hip (8 independent FMA chains per lane, 8 waves/SIMD):
+# scalar v_fma_f32 and packed v_pk_fma_f32 (the spec figure counts the packed form)
+FP32_MEASURED_TFLOPS = {"v_fma_f32": 73.8, "v_pk_fma_f32": 143.0}
 
 CONFIGS = {
     "c1": dict(scene="sphere1.scene", W=256, H=256, spp=1, bounces=1, name="C1 single-sphere SDF"),
@@ -461,6 +464,8 @@ def main():
                 traffic = None
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "peak_measured": dict(FP32_MEASURED_TFLOPS, source="tools/probes/fma_peak.hip"),
+                "frac_of_measured_scalar_fma": round(achieved / FP32_MEASURED_TFLOPS["v_fma_f32"], 4),
                 "kernel": ("rmr_jit_trace (hipRTC scene-specialised trace kernel)" if st.jit_launches
                            else "k_trace<RM1,persistent>"), "avg_launch_ms": round(per_launch_ms, 3),
                 "map_evals_per_launch": int(st.map_evals / st.trace_launches),
