@@ -662,8 +662,8 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 // Where the cached primitives are read from: the leaf-ordered DPrim table itself (global, per-lane
 // vector loads through the L1) or, with RMR_NPC_LDS, a copy of it staged in the workgroup's LDS at
 // kernel start (scenes of <= RMR_NPC_LDS_MAX primitives).
-// (csg256 8 spp: 26.2 -> 25.6 ms with the table in LDS and 32-unit chunks, which keep the block's LDS
-// at 20 KiB = 8 blocks per CU; with 64-unit chunks the LDS cost two waves per SIMD: slower)
+// (csg256 8 spp at 6 waves / SIMD: 24.0 -> 22.2 ms with the table in LDS; at 8 waves the block's LDS
+// had to stay at 20 KiB for 8 blocks per CU)
 #ifndef RMR_NPC_LDS
 #define RMR_NPC_LDS 1
 #endif
@@ -1971,6 +1971,12 @@ RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_N
 #ifndef RMR_GENERAL_WAVES
 #define RMR_GENERAL_WAVES 8
 #endif
+// waves/SIMD of the nearest-primitive cache kernels (BVH scenes): at 8 the allocator spills hot march
+// state (origin, escape bound) inside the cache loop, reloaded every iteration; at 6 it does not
+// (csg256 8 spp: 8 / 7 / 6 / 5 waves -> 25.3 / 23.5 / 22.2 (64-unit chunks) / 24.3 ms)
+#ifndef RMR_CACHE_WAVES
+#define RMR_CACHE_WAVES 6
+#endif
 template <int VAR, bool GENERAL, bool PROG>
 constexpr int trace_waves() {
     return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
@@ -1988,7 +1994,7 @@ constexpr int trace_waves() {
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
 #ifndef RMR_CHUNK_CACHE
-#define RMR_CHUNK_CACHE 32   // the same for the nearest-primitive cache kernels (LDS budget, RMR_NPC_LDS)
+#define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
 #ifndef RMR_INNER_MARCH
 #define RMR_INNER_MARCH 1
