@@ -77,6 +77,12 @@ def parse():
                          "0: one context; default: on for N > 1")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="GPU rehearsal of the multi-rank path on a one-GPU box: every rank renders on "
+                         "cuda:0 with the HIP kernels, the frame reduce runs over gloo (staged through "
+                         "host memory); a correctness rehearsal, not a scaling measurement")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N > 1: skip rank 0's check of the last reduced frame against a one-context render")
     return ap.parse_args()
 
 
@@ -263,6 +269,55 @@ def spawn_ranks(n):
     return bad[0] if bad else 0
 
 
+class _StagedDist:
+    """torch.distributed for the --share-gpu rehearsal: gloo reduces host tensors, so the frame
+    reduce copies the accumulator to the host on the caller's current stream (which waits for the
+    render enqueued on it), reduces there and copies the sum back. Everything else is the real
+    module."""
+
+    def __init__(self, dist):
+        self._d = dist
+
+    def __getattr__(self, k):
+        return getattr(self._d, k)
+
+    def reduce(self, t, dst=0, op=None, group=None, async_op=False):
+        import torch
+        host = t.cpu()   # synchronous on the current stream
+        self._d.reduce(host, dst=dst, op=op if op is not None else self._d.ReduceOp.SUM, group=group)
+        if self._d.get_rank(group) == dst:
+            t.copy_(host.to(t.device))
+        torch.cuda.current_stream().synchronize()
+        return _DoneWork() if async_op else None
+
+
+class _DoneWork:
+    def wait(self):
+        return True
+
+
+def verify_last_frame(cfg, fr, times, scene, spp, device):
+    """Rank 0, after the timed region: the last reduced frame against a one-context render of the
+    whole frame (same scene, same seeds) — bitwise, since every rank's accumulator is zero outside
+    its tiles and x + 0 = x."""
+    import numpy as np
+    from raymarchrenderer_amd import Renderer, abi
+    from raymarchrenderer_amd.multi_gpu import frame_tiles
+    W, H = cfg["W"], cfg["H"]
+    got = fr.last.cpu().numpy()
+    r = Renderer(device, W, H)
+    try:
+        r.load_scene(scene, "rm1")
+        r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
+        r.render_tiles(times, frame_tiles(W, H, TILE), TILE)
+        want = r.read_accum()
+    finally:
+        r.close()
+    diff = got.view(np.uint32) != want.view(np.uint32)
+    return {"bitwise_equal_to_one_context": bool(not diff.any()), "differing_words": int(diff.sum()),
+            "frame_spp": spp}
+
+
 DRY_W, DRY_H, DRY_TILE, DRY_SPP = 64, 48, 16, 2
 
 
@@ -335,9 +390,16 @@ def main():
     spp = args.spp or cfg["spp"]
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
     dist_on = world > 1
-    if dist_on:
+    if args.share_gpu:
+        # every rank on the one GPU; RCCL refuses two ranks on one device, so the reduce runs over
+        # gloo through host memory (_StagedDist). The render path is the product's.
+        local_rank = 0
+    torch.cuda.set_device(local_rank)
+    if dist_on and args.share_gpu:
+        dist.init_process_group("gloo")
+        dist = _StagedDist(dist)
+    elif dist_on:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     from raymarchrenderer_amd import Renderer, abi, time_schedule
     from raymarchrenderer_amd.multi_gpu import FrameRenderer, reduce_frame
@@ -377,15 +439,17 @@ def main():
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
     static_times = time_schedule(spp)
     frame_no = [0]
+    last = {}
 
     def step():
         f = frame_no[0]
         frame_no[0] += 1
         if animated:
-            fr.next_renderer().load_scene(scene_for_frame(cfg, f % 120), "rm1")
-            fr.frame(time_schedule(spp, frame=f % 120))
+            last["scene"], last["times"] = scene_for_frame(cfg, f % 120), time_schedule(spp, frame=f % 120)
+            fr.next_renderer().load_scene(last["scene"], "rm1")
         else:
-            fr.frame(static_times)
+            last["scene"], last["times"] = scene_for_frame(cfg, 0), static_times
+        fr.frame(last["times"])
 
     for _ in range(args.warmup):
         step()
@@ -407,9 +471,13 @@ def main():
     st = combined_stats(rs)
     per_rank = None
     reduce_ms = None
+    verify = None
     if dist_on:
+        if rank == 0 and not args.no_verify:
+            verify = verify_last_frame(cfg, fr, last["times"], last["scene"], spp, local_rank)
         mine = torch.tensor([elapsed, st.trace_ms, float(st.trace_launches), float(st.map_evals),
-                             float(len(fr.tiles))], dtype=torch.float64, device="cuda")
+                             float(len(fr.tiles))], dtype=torch.float64,
+                            device="cpu" if args.share_gpu else "cuda")
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         allr = [a.cpu().tolist() for a in allr]
@@ -501,10 +569,15 @@ def main():
                           "frame_streams": n_ctx},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity}
         if dist_on:
-            out["multi_gpu"] = {"backend": "nccl (RCCL)", "partition": "32x32 tiles round-robin",
+            out["multi_gpu"] = {"backend": "gloo via host (--share-gpu rehearsal)" if args.share_gpu else "nccl (RCCL)",
+                                "partition": "32x32 tiles round-robin",
                                 "collective": "one reduce(SUM) of the %.1f MB RGBA32F frame per step"
                                               % (W * H * 16 / 1e6),
-                                "reduce_ms_standalone": round(reduce_ms, 3), "per_rank": per_rank}
+                                "reduce_ms_standalone": round(reduce_ms, 3), "per_rank": per_rank,
+                                "verify": verify}
+            if args.share_gpu:
+                out["n_gpus"] = 1
+                out["rehearsal"] = "%d ranks sharing one GPU: a correctness rehearsal, not a measurement" % world
         print(json.dumps(out), flush=True)
     for r in rs:
         r.close()

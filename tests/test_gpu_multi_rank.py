@@ -1,0 +1,43 @@
+"""bench.py's multi-rank path on a GPU: `--gpus N --share-gpu` starts N rank processes that all render
+with the HIP kernels on cuda:0 (each rank two renderer contexts on two torch streams, frames pipelined
+over two accumulators, exactly the N > 1 schedule) and reduce each frame over gloo through host
+memory (RCCL refuses two ranks on one device; the driver's 8-GPU run uses RCCL). Rank 0 checks the
+last reduced frame bit for bit against a one-context render of the whole frame.
+
+This is the GPU rehearsal of what the driver's scaling run does on 8 GPUs: rank spawning before any
+GPU call, per-rank streams, the zero / render / reduce ordering (a renderer on a private
+non-blocking stream would race the zeroing and the reduce), and the tile partition."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args, timeout=240):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + list(args), capture_output=True,
+                       text=True, timeout=timeout, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus,config,spp", [(2, "c2", 4), (3, "c5", 2)])
+def test_share_gpu_ranks_reduce_bitexact(gpus, config, spp):
+    out = _run("--gpus", str(gpus), "--share-gpu", "--config", config, "--spp", str(spp), "--steps", "3",
+               "--warmup", "1", "--no-cpu-baseline", "--no-psnr", "--no-count-pass")
+    mg = out["multi_gpu"]
+    assert len(mg["per_rank"]) == gpus
+    assert all(p["trace_launches"] > 0 for p in mg["per_rank"])
+    assert sum(p["tiles32"] for p in mg["per_rank"]) == 60 * 34
+    assert mg["verify"]["bitwise_equal_to_one_context"] is True, mg["verify"]
+    assert out["config"]["frame_streams"] == 2
