@@ -1219,51 +1219,21 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
 // which the NaN-dropping fminf/fmaxf ignore (the ray then lies on a box face: >= the inflation
 // from every primitive). A NaN origin or direction (e.g. randHemisphere about a normal of exactly
 // (0,-1,0)) never escapes: the reference's map(NaN) "hits" at t = 0 (opU NaN rule).
-#ifndef RMR_ESC_FMA
-#define RMR_ESC_FMA 0
-#endif
-template <bool FMA>
-RMR_D float ray_exit_boxes(const KParams& P, V3 o, float ix, float iy, float iz) {
+RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
+    const float chk = ((o.x + o.y) + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
+    if (!P.esc_on || !(chk == chk)) return __builtin_inff();
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     float last = -__builtin_inff();
-    // FMA: slab parameters as fma(B, 1/d, -o/d), one instruction per face instead of two (callers
-    // ensure o/d is finite). The error is a coordinate error: the point at the computed parameter
-    // is within 2^-23 (|o| + |B|) of the face along that axis, far inside the inflation's
-    // 2^-16 (|eye| + 2E + 3 maxDist)
-    const float nox = -(o.x * ix), noy = -(o.y * iy), noz = -(o.z * iz);
     for (int b = 0; b < P.n_esc; b++) {
         const float* B = P.esc_boxes + 6 * b;   // wave-uniform: scalar loads
-        float ax, bx, ay, by, az, bz;
-        if constexpr (FMA) {
-            ax = fmaf(B[0], ix, nox), bx = fmaf(B[3], ix, nox);
-            ay = fmaf(B[1], iy, noy), by = fmaf(B[4], iy, noy);
-            az = fmaf(B[2], iz, noz), bz = fmaf(B[5], iz, noz);
-        } else {
-            ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
-            ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
-            az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
-        }
+        const float ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
+        const float ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
+        const float az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
         const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
         // inside this box for t in [tn, tf] (nonempty and ahead): the ray may still hit its primitives
         if (!(tn > tf)) last = fmaxf(last, tf);
     }
-    return last;
-}
-RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
-    const float chk = ((o.x + o.y) + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
-    if (!P.esc_on || !(chk == chk)) return __builtin_inff();
-    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
-    float last;
-#if RMR_ESC_FMA
-    // o/d must be finite for the fma form (a zero or tiny direction component: 1/d = +-inf or o/d
-    // overflows); those rare lanes take the subtract-multiply form, where (B - o) * inf keeps the slab's
-    // "no constraint / never inside" meaning
-    const float q = fabsf(o.x * ix) + (fabsf(o.y * iy) + fabsf(o.z * iz));
-    if (__builtin_expect(q < __builtin_inff(), 1)) last = ray_exit_boxes<true>(P, o, ix, iy, iz);
-    else last = ray_exit_boxes<false>(P, o, ix, iy, iz);
-#else
-    last = ray_exit_boxes<false>(P, o, ix, iy, iz);
-#endif
     // relative error < 2^-21: widen a positive bound
     return last > 0.0f ? fmaf(last, 1.0f + 0x1p-19f, 0x1p-60f) : last;
 }
