@@ -39,14 +39,15 @@ typedef const __attribute__((address_space(4))) DPrim CDPrim;
 #define PI_F 3.14159274101257324219f
 
 enum Phase : int {
-    PH_IDLE = 0,
-    PH_MARCH = 1,   // march() step of the primary / bounce ray
-    PH_NORMAL = 2,  // getNormal() probe 0..5
-    PH_SHADOW = 3,  // RM2 light-march step
-    PH_HIT = 4,     // march hit, normal ready: run the material
-    PH_MISS = 5,    // march miss: sky
-    PH_NEE = 6,     // RM2: shadow march finished
-    PH_RESTART = 7, // separateChannels: next channel's trace starts at the next refill point
+    // the three marching phases first: is_active is one unsigned compare
+    PH_MARCH = 0,   // march() step of the primary / bounce ray
+    PH_NORMAL = 1,  // getNormal() probe 0..5
+    PH_SHADOW = 2,  // RM2 light-march step
+    PH_HIT = 3,     // march hit, normal ready: run the material
+    PH_MISS = 4,    // march miss: sky
+    PH_NEE = 5,     // RM2: shadow march finished
+    PH_RESTART = 6, // separateChannels: next channel's trace starts at the next refill point
+    PH_IDLE = 7,
 };
 
 // Per-lane path state. Kept small on purpose (the fast kernels run 8 waves/SIMD = 64 VGPRs):
@@ -483,12 +484,22 @@ RMR_D void am_sphere(AMin& m, V3 p, V3 c, float r, float id) {
 struct BMin {
     float k1, k2, id;
 };
+#ifndef RMR_BKEY_ADD
+#define RMR_BKEY_ADD 1
+#endif
 RMR_D float bm_key(V3 p, V3 c, V3 r) {
     const V3 q = vabs(p - c) - r;
     const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
     const V3 o = vmax0(q);
     const float l2 = dot(o, o);
+#if RMR_BKEY_ADD
+    // one of the two is zero (outside: max q > 0, so k = 0; inside: every q <= 0, so len2 = 0; a
+    // positive q whose square underflows gives 0 + 0), so l2 + k is exactly the selected key, NaN for
+    // a NaN point; only -0 becomes +0, which orders, folds and square-roots the same
+    return l2 + k;
+#else
     return (l2 > 0.0f || l2 != l2) ? l2 : k;
+#endif
 }
 RMR_D void bm_box0(BMin& b, V3 p, V3 c, V3 r, float id) {
     b.k1 = bm_key(p, c, r);
@@ -1954,8 +1965,8 @@ RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
     L.bounces = cb >> 8;
 }
 
-RMR_D bool is_active(int ph) { return ph == PH_MARCH || ph == PH_NORMAL || ph == PH_SHADOW; }
-RMR_D bool is_shade(int ph) { return ph == PH_HIT || ph == PH_MISS || ph == PH_NEE; }
+RMR_D bool is_active(int ph) { return (uint32_t)ph <= (uint32_t)PH_SHADOW; }   // PH_DONE (-1) is not
+RMR_D bool is_shade(int ph) { return (uint32_t)(ph - PH_HIT) <= (uint32_t)(PH_NEE - PH_HIT); }
 
 // ------------------------------------------------------------------------------------------
 // the trace kernel
@@ -2251,6 +2262,8 @@ RMR_D void trace_main(const KParams& P) {
             // map() steps back to back until a shading batch is due or no lane is active: idle lanes
             // only appear in shading and refill, so the refill / restart checks can wait until then
             uint64_t am = amask;
+            // the loop's own counts (scalar registers; the wave counters were carried in VGPRs here)
+            uint32_t lmaps = 0, liters = 0;
             for (;;) {
                 if (is_active(L.phase)) {
                     const V3 p = RMR_MARCH_POINT(L);
@@ -2260,13 +2273,15 @@ RMR_D void trace_main(const KParams& P) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO>(P, L, m);
                 }
-                maps += (WCount)__popcll(am);
-                iters++;
+                lmaps += (uint32_t)__popcll(am);
+                liters++;
                 if (!RMR_INNER_MARCH) break;
                 const uint64_t sm = __ballot(is_shade(L.phase));
                 am = __ballot(is_active(L.phase));
                 if (!am || __popcll(sm) >= T) break;
             }
+            maps += (WCount)__builtin_amdgcn_readfirstlane(lmaps);
+            iters += (WCount)__builtin_amdgcn_readfirstlane(liters);
         }
         RMR_STAMP(c2);
         const uint64_t smask = __ballot(is_shade(L.phase));
