@@ -523,7 +523,10 @@ RMR_D void am_boxes(AMin& m, const BMin& b) {
 // for a minimiser whose len2 is in sqrt_cr's tiny range (0 < len2 < 2^-96: the exact fold handles it)
 RMR_D bool am_unique(const AMin& m, float R2) {   // R2 = 2 R
     const float margin = fmaf(fabsf(m.a) + fabsf(m.s2) + R2, 0x1p-20f, 0x1p-39f);
-    return m.s2 - m.a > margin && (m.l2 >= 0x1p-96f || m.l2 == 0.0f);
+    // len2 (never negative; a NaN one fails the gap test) is +0 or >= 2^-96: one unsigned compare,
+    // and both tests without a short-circuit branch
+    const bool big = (__float_as_uint(m.l2) - 1u) >= (__float_as_uint(0x1p-96f) - 1u);
+    return (m.s2 - m.a > margin) & big;
 }
 // exact result of a unique fold: opU((maxDist, -1), d_w, id_w); d_w = sqrt_cr(len2) + k is the same
 // expression as sd_box (k + length) and sd_sphere (length - r == length + (-r)). sqrt_cr_big: the
@@ -1543,15 +1546,18 @@ RMR_D V3 march_point(const Lane& L) {
     const float T = nrm ? 1.0f : L.t;
     return vfma(D, T, HO ? L.o : (nrm ? L.hit : L.o));
 }
-// nrm.c holds map(p + h e_c) after the + probe and map(p + h e_c) - map(p - h e_c) after the - probe
+// getNormal's differences map(p + h e_c) - map(p - h e_c) through a shift register: a + probe parks
+// its value in nrm.z; a - probe forms the difference (the same one subtraction) and, for x and y,
+// shifts it in (nrm.x <- nrm.y, nrm.y <- difference), for z leaves it in nrm.z. After the six probes
+// nrm = (dx, dy, dz); one value per lane changes per probe instead of a per-axis select of all three.
 RMR_D void normal_update(Lane& L, float m) {
-    const int ax = L.ctr >> 1;
     const bool plus = (L.ctr & 1) == 0;
-    // (no select between struct fields here: clang turns that into a dynamic stack index)
-    const float vx = plus ? m : L.nrm.x - m, vy = plus ? m : L.nrm.y - m, vz = plus ? m : L.nrm.z - m;
-    L.nrm.x = ax == 0 ? vx : L.nrm.x;
-    L.nrm.y = ax == 1 ? vy : L.nrm.y;
-    L.nrm.z = ax == 2 ? vz : L.nrm.z;
+    const bool last = L.ctr == 5;
+    const float dv = L.nrm.z - m;
+    const bool shift = !plus && !last;
+    L.nrm.x = shift ? L.nrm.y : L.nrm.x;
+    L.nrm.y = shift ? dv : L.nrm.y;
+    L.nrm.z = plus ? m : (last ? dv : L.nrm.z);
     L.ctr++;
     if (L.ctr == 6) L.phase = PH_HIT;   // normalize() happens in the shading batch (shade())
 }
