@@ -39,15 +39,15 @@ typedef const __attribute__((address_space(4))) DPrim CDPrim;
 #define PI_F 3.14159274101257324219f
 
 enum Phase : int {
-    // the three marching phases first: is_active is one unsigned compare
+    // marching phases first and shading phases last: is_active and is_shade are one compare each
     PH_MARCH = 0,   // march() step of the primary / bounce ray
     PH_NORMAL = 1,  // getNormal() probe 0..5
     PH_SHADOW = 2,  // RM2 light-march step
-    PH_HIT = 3,     // march hit, normal ready: run the material
-    PH_MISS = 4,    // march miss: sky
-    PH_NEE = 5,     // RM2: shadow march finished
-    PH_RESTART = 6, // separateChannels: next channel's trace starts at the next refill point
-    PH_IDLE = 7,
+    PH_IDLE = 3,
+    PH_RESTART = 4, // separateChannels: next channel's trace starts at the next refill point
+    PH_HIT = 5,     // march hit, normal ready: run the material
+    PH_MISS = 6,    // march miss: sky
+    PH_NEE = 7,     // RM2: shadow march finished
 };
 
 // Per-lane path state. Kept small on purpose (the fast kernels run 8 waves/SIMD = 64 VGPRs):
@@ -1972,7 +1972,7 @@ RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
 }
 
 RMR_D bool is_active(int ph) { return (uint32_t)ph <= (uint32_t)PH_SHADOW; }   // PH_DONE (-1) is not
-RMR_D bool is_shade(int ph) { return (uint32_t)(ph - PH_HIT) <= (uint32_t)(PH_NEE - PH_HIT); }
+RMR_D bool is_shade(int ph) { return ph >= PH_HIT; }   // (PH_DONE, -1, is not)
 
 // ------------------------------------------------------------------------------------------
 // the trace kernel
