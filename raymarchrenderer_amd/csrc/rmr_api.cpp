@@ -380,14 +380,14 @@ int ensure_jit(rmr_ctx* c) {
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = split ? 2 : 4;
     k.blocks_per_cu = b;
-    // RM1 inline sphere/box maps: 20 (C2 +2%); general maps without material programs, whose
-    // map() dwarfs the shading (the Mandelbulb): 8 (C3 +2-3%); otherwise 16
+    // general maps without material programs, whose map() dwarfs the shading (the Mandelbulb): 8
+    // (C3 +2-3%); otherwise 16 (RM1 inline sphere/box maps: 20 until the map() loop lost ~12% of its
+    // instructions in round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default
+    // +1.2%, tools/env_ab.py shade_t)
     // split kernels: lanes a marching wave collects before handing finished marches over (and idle
     // lanes before it refills)
     if (split)
         k.shade_t = 6;
-    else if (src.find("rmr::trace_waves<1, false, false>") != std::string::npos && src.find("TableMap<") == std::string::npos)
-        k.shade_t = 20;
     else if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
         k.shade_t = 8;
     else
