@@ -72,6 +72,21 @@ RMR_D float sqrt_cr_big(float x) {
     float s = (rm <= 0.0f) ? sm : s0;
     return (rp > 0.0f) ? sp : s;
 }
+// Correctly rounded reciprocal and quotient without the IEEE division sequence (div_scale / fmas /
+// fixup), for operands the caller keeps in range: v_rcp_f32 (<= 1 ulp) plus one Newton step gives
+// RN(1/b) for |b| in [2^-125, 2^125]; Markstein's correction q' = RN(q + RN(a - b q) y) of
+// q = RN(a y), y = RN(1/b), is RN(a / b) when nothing over- or underflows. Verified on the box
+// (tools/probes/div_markstein.hip): every b of that range, every a of the Mandelbulb iteration's
+// sqrt(a) / a^4, and 2^34 random pairs.
+RMR_D float rcp_cr(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return fmaf(fmaf(-b, r, 1.0f), r, r);
+}
+RMR_D float div_mk(float a, float b) {
+    const float y = rcp_cr(b);
+    const float q = a * y;
+    return fmaf(fmaf(-b, q, a), y, q);
+}
 RMR_D float length(V3 a) { return sqrt_cr(dot(a, a)); }
 RMR_D V3 normalize(V3 a) { float inv = 1.0f / length(a); return a * inv; }
 RMR_D V3 vfma(V3 a, float s, V3 b) { return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z)); }

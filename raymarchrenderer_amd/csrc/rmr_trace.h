@@ -220,6 +220,9 @@ RMR_D void mb_iter8(V3& z, float& dr, V3 p0, float r) {
 #ifndef RMR_MB_POLY
 #define RMR_MB_POLY 1
 #endif
+#ifndef RMR_MB_DIVMK
+#define RMR_MB_DIVMK 1   // sqrt(a) / a^4 by div_mk (rmr_math.h) instead of the IEEE division sequence
+#endif
 RMR_D void mb_iter8_poly(V3& z, float& dr, V3 p0, float r) {
     const float c = z.x * z.x, d = z.y * z.y, b = z.z * z.z;
     const float a = c + d;
@@ -237,7 +240,16 @@ RMR_D void mb_iter8_poly(V3& z, float& dr, V3 p0, float r) {
     const float re8p = fmaf(re4p, re4p, -(im4p * im4p));              // a^4 cos 8 phi
     const float im8p = (2.0f * re4p) * im4p;                          // a^4 sin 8 phi
     const float a2 = a * a;
+#if RMR_MB_DIVMK
+    // a >= 2^-30 here (and a <= bail^2); for a <= 2^31 the quotient and its residual stay normal
+    // (div_mk's range): the IEEE division only in a wave with a lane beyond that (bail > 2^15.5)
+    const float sa = sqrt_cr_big(a), a4 = a2 * a2;
+    float w;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(a <= 0x1p31f)) == 0, 1)) w = div_mk(sa, a4);
+    else w = (a <= 0x1p31f) ? div_mk(sa, a4) : sa / a4;
+#else
     const float w = sqrt_cr(a) / (a2 * a2);
+#endif
     const float t = (((8.0f * z.z) * bma) * re4) * w;                 // r^8 sin 8 theta / a^4
     const float r2 = r * r, r4 = r2 * r2, r7 = (r4 * r2) * r;
     dr = fmaf(8.0f * r7, dr, 1.0f);
