@@ -230,12 +230,12 @@ int rmr_set_schedule(rmr_ctx* ctx, int schedule);
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);
 /* Tuning knobs (<= 0 / < 0 keeps the current value): deferred-shading batch size in lanes (1..64),
  * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. Until a
- * batch size is set (here or by env RMR_SHADE_T) it is chosen per kernel: 20 for RM1 sphere/box
- * specialisations, 8 for general maps without material programs, 16 otherwise. Results do not
- * depend on any of these (scheduling only). */
+ * batch size is set (here or by env RMR_SHADE_T) it is chosen per kernel: 8 for general maps
+ * without material programs, 16 otherwise. Results do not depend on any of these (scheduling only). */
 int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long samp_budget_bytes);
 /* (shade_threshold bits 8..15, when non-zero, set the refill threshold separately: idle lanes a
- * wave collects before it fetches new units; default = the shading threshold.) */
+ * wave collects before it fetches new units; default (and when zero) = half the shading
+ * threshold, at least 2; env RMR_REFILL_T=0 makes it the shading threshold.) */
 /* Test hook: per-sample radiance (before the running mean) of the integer rect, written as
  * out[k][y-y0][x-x0][4]; sample k is seeded with times[k]. The accumulator is left unchanged. */
 int rmr_trace_samples(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out);

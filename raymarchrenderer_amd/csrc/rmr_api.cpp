@@ -101,7 +101,10 @@ struct rmr_ctx {
     int kernel_mode = 0;  // 0 persistent, 1 thread-per-path
     int shade_threshold = 16;   // explicit (env RMR_SHADE_T / rmr_set_tuning) or, with shade_auto, per kernel:
     bool shade_auto = true;     // per specialised kernel (ensure_jit: 20 / 8 / 16), 16 for the table kernels
-    int refill_threshold = 2;   // 0 = shade_threshold (tuned on C2: T=16; refills are cheap with LDS chunk rays)
+    // idle lanes before a refill: -1 = half the shading threshold, at least 2 (round 2: T/2 = 8 at T = 16:
+    // Cornell-5 -0.4%, RM3 -1.2%, default -2% against 2; Mandelbulb T = 8: 4 best); 0 = the shading
+    // threshold; refills are cheap with the LDS chunk rays
+    int refill_threshold = -1;
     // nearest-primitive cache: 40 lanes per full map() batch, or once waiting lanes >= cache-served ones
     // (R = 8; csg256 with the candidate grid: 15.7 -> 14.8 ms per 4 spp against R = 2)
     int full_threshold = 40 | (8 << 8);
@@ -124,6 +127,14 @@ struct rmr_ctx {
 };
 
 namespace {
+
+// the kernel's refill threshold from the context setting (rmr_ctx::refill_threshold) and the
+// shading threshold in effect
+int refill_for(int setting, int shade_t) {
+    if (setting > 0) return setting;
+    if (setting == 0) return shade_t;
+    return std::max(2, shade_t / 2);
+}
 
 int fail(rmr_ctx* c, int code, const std::string& m) {
     if (c) c->err = m;
@@ -721,7 +732,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.flops_static = (int32_t)s.flops_per_map();
     P.transc_static = (int32_t)s.transc_per_map();
     P.shade_threshold = c->shade_threshold;
-    P.refill_threshold = c->refill_threshold > 0 ? c->refill_threshold : c->shade_threshold;
+    P.refill_threshold = refill_for(c->refill_threshold, c->shade_threshold);
 
     // hipRTC specialisation for large launches (always when jit_mode == 1)
     bool use_jit = false;
@@ -757,7 +768,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         // and the cached BVH map -1..2%)
         if (c->shade_auto) {
             P.shade_threshold = use_jit ? c->jit.shade_t : 16;
-            P.refill_threshold = c->refill_threshold > 0 ? c->refill_threshold : P.shade_threshold;
+            P.refill_threshold = refill_for(c->refill_threshold, P.shade_threshold);
         }
         HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(unsigned long long), c->stream));
         EventPair ev = get_events(c);
@@ -1324,7 +1335,8 @@ int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long s
     if (shade_threshold > 0) {
         c->shade_threshold = std::max(1, std::min(64, shade_threshold & 0xff));
         c->shade_auto = false;
-        c->refill_threshold = std::min(64, (shade_threshold >> 8) & 0xff);
+        const int tr = (shade_threshold >> 8) & 0xff;
+        c->refill_threshold = tr ? std::min(64, tr) : -1;   // unset: half the shading threshold
     }
     if (grid_per_cu >= 0) c->grid_per_cu = grid_per_cu;
     if (samp_budget_bytes > 0) c->samp_budget = (size_t)samp_budget_bytes;
