@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--shade-threshold", type=int, default=0)
     ap.add_argument("--traffic-json", default="")
     ap.add_argument("--overlap", type=int, default=-1,
-                    help="1: two renderer contexts on two streams, consecutive frames overlap on the GPU "
+                    help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU "
                          "(measured +0.9%% at N=1; the per-launch event times then include waiting); "
                          "0: one context; default: on for N > 1")
     ap.add_argument("--dry-run", action="store_true",
@@ -409,7 +409,7 @@ def main():
     # one frame's trace-kernel drain overlaps the next frame's start (multi_gpu.FrameRenderer).
     # Default on for N > 1 (a rank's frame is 1/N as long, the drain is not).
     overlap = args.overlap if args.overlap >= 0 else int(dist_on)
-    n_ctx = 2 if overlap else 1
+    n_ctx = overlap + 1 if overlap > 0 else 1
     rs, streams = [], []
     for _ in range(n_ctx):
         r = Renderer(local_rank, W, H)
@@ -433,7 +433,7 @@ def main():
         r.set_stream(s_.cuda_stream)
         rs.append(r)
         streams.append(s_)
-    n_acc = 2 if (dist_on or n_ctx > 1) else 1
+    n_acc = n_ctx if n_ctx > 1 else (2 if dist_on else 1)
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_acc)]
     torch.cuda.synchronize()
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
