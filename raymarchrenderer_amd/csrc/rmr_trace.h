@@ -2084,6 +2084,11 @@ RMR_D void trace_main(const KParams& P) {
 #endif
     const int wv = (threadIdx.x >> 6) & 3;
     uint32_t chunk_base = 0;
+#ifdef RMR_WAVE_TIMES   // counters [9] ~min start, [11] ~min / [10] max queue exhaustion, [12] ~min /
+                        // [13] max end, [15] sum over waves of end - exhaustion (s_memrealtime ticks)
+    unsigned long long t_exh = 0;
+    if (__lane_id() == 0) atomicMax(P.counters + 9, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     for (;;) {
         RMR_STAMP(c0);
         bool fresh = false;
@@ -2099,6 +2104,14 @@ RMR_D void trace_main(const KParams& P) {
                     rnext = base;
                     exhausted = base >= n_units;
                     rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
+#ifdef RMR_WAVE_TIMES   // diagnostics (tools/wave_times.py): when each wave finds the queue empty
+                    if (exhausted && __lane_id() == 0) {
+                        const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+                        t_exh = te;
+                        atomicMax(P.counters + 11, ~te);
+                        atomicMax(P.counters + 10, te);
+                    }
+#endif
                     if (!exhausted) {  // the chunk's primary rays, all 64 lanes at once
                         chunk_base = base;
                         for (uint32_t sl = __lane_id(); sl < CHUNK; sl += 64) {
@@ -2334,6 +2347,14 @@ RMR_D void trace_main(const KParams& P) {
         }
         if (last) break;
     }
+#ifdef RMR_WAVE_TIMES
+    if (__lane_id() == 0) {
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        atomicMax(P.counters + 12, ~tn);
+        atomicMax(P.counters + 13, tn);
+        if (t_exh) atomicAdd(P.counters + 15, tn - t_exh);
+    }
+#endif
     if (__lane_id() == 0) {
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
