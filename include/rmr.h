@@ -200,7 +200,7 @@ int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double 
  * the scene's map() is generated as HIP source with the primitives as literals and compiled by
  * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under
  * $RMR_JIT_CACHE or ~/.cache/rmr-jit). Results are bit-identical to the table-driven kernels.
- * mode 0 = off, 1 = always (errors are returned), 2 = auto (default: launches of >= 2^20 units;
+ * mode 0 = off, 1 = always (errors are returned), 2 = auto (default: launches of >= 2^16 units;
  * a failed compile falls back to the table-driven kernel). Env RMR_JIT overrides at rmr_create. */
 int rmr_set_jit(rmr_ctx* ctx, int mode);
 /* Exact work-skipping in the trace kernels (all results bit-identical; only the count of map()
