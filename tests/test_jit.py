@@ -42,6 +42,19 @@ def test_jit_source_compiles_for_gfx950(tmp_path, monkeypatch, name, path, varia
     assert jit_compile_scene(path, variant) == key   # cached, same key
 
 
+def test_jit_scheduler_directive(tmp_path, monkeypatch):
+    """The inline approximate-map kernels (Cornell-5) carry an `//@opts` scheduler directive
+    (rmr_jit.cpp): it reaches hipRTC (another code object under another key); RMR_JIT_SCHED=0 drops it."""
+    path = os.path.join(SCENES, "cornell5.scene")
+    monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path))
+    k_on = jit_compile_scene(path, "rm1")
+    monkeypatch.setenv("RMR_JIT_SCHED", "0")
+    k_off = jit_compile_scene(path, "rm1")
+    assert k_on != k_off
+    on, off = (tmp_path / (k_on + ".hsaco")).read_bytes(), (tmp_path / (k_off + ".hsaco")).read_bytes()
+    assert on != off
+
+
 def _setup(r, path, variant, W, H, overrides):
     r.set_image_size(W, H)
     r.reload()
