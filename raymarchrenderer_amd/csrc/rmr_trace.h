@@ -81,7 +81,10 @@ struct Lane {
     int cw, cw2;   // (cw2: the second cached primitive when RMR_NPC_K == 2, else == cw)
     float cs, cta;
     float texit;   // escape bound of the current ray (ray_exit)
+    V3 e;          // HO kernels: the getNormal probe offset of probe ctr (normal_update cycles it)
 };
+// the first probe's offset (+h, +0, +0); the six-probe cycle of normal_update returns to it
+RMR_D void init_probe(Lane& L) { L.e = v3(0.001f, 0.0f, 0.0f); }
 template <bool HO> RMR_D V3& hitref(Lane& L) {
     if constexpr (HO) return L.o;
     else return L.hit;
@@ -1548,13 +1551,11 @@ RMR_D V3 probe_point(const Lane& L) {
 }
 // The map() point of an active lane without a divergent branch: march points are fma(d, t, o); a
 // probe is hit + e as fma(e, 1, hit), which is the same rounded add bit for bit (e * 1 is exact).
+// The probe offset is the lane's e (normal_update), equal to probe_point's offset for ctr.
 template <bool HO>
 RMR_D V3 march_point(const Lane& L) {
     const bool nrm = (L.phase == PH_NORMAL);
-    const int ax = L.ctr >> 1;
-    const bool neg = (L.ctr & 1) != 0;
-    const float h = 0.001f, hs = neg ? -h : h, z0 = neg ? -0.0f : 0.0f;
-    const V3 D = nrm ? v3(ax == 0 ? hs : z0, ax == 1 ? hs : z0, ax == 2 ? hs : z0) : L.d;
+    const V3 D = nrm ? L.e : L.d;
     const float T = nrm ? 1.0f : L.t;
     return vfma(D, T, HO ? L.o : (nrm ? L.hit : L.o));
 }
@@ -1570,6 +1571,10 @@ RMR_D void normal_update(Lane& L, float m) {
     L.nrm.x = shift ? L.nrm.y : L.nrm.x;
     L.nrm.y = shift ? dv : L.nrm.y;
     L.nrm.z = plus ? m : (last ? dv : L.nrm.z);
+    // next probe offset: after a + probe its negation (-h, -0, -0 for x), after a - probe the next
+    // axis's + probe, (-e.z, -e.x, -e.y): (-h,-0,-0) -> (+0,+h,+0) -> (-0,-h,-0) -> (+0,+0,+h) ->
+    // (-0,-0,-h) -> (+h,+0,+0), the first probe of the next normal. Signed zeros as probe_point's.
+    L.e = plus ? -L.e : v3(-L.e.z, -L.e.x, -L.e.y);
     L.ctr++;
     if (L.ctr == 6) L.phase = PH_HIT;   // normalize() happens in the shading batch (shade())
 }
@@ -2041,6 +2046,7 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
+    init_probe(L);
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
     WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, steps = 0;
@@ -2566,6 +2572,7 @@ RMR_D void split_shade(const KParams& P, SplitLds& S) {
     Lane L;
     L.phase = PH_IDLE;
     L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
+    init_probe(L);
     const uint64_t n_units = P.n_units;
     const uint32_t cap = 64u * RMR_SPLIT_WAVES + 2u * kSplitMarch * RMR_SPLIT_RING - 1u;
     const uint32_t target = (uint32_t)RMR_SPLIT_INFLIGHT < cap ? (uint32_t)RMR_SPLIT_INFLIGHT : cap;
@@ -2744,6 +2751,7 @@ RMR_D void split_march(const KParams& P, SplitLds& S, int w) {
     Lane L;
     L.phase = PH_IDLE;
     L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
+    init_probe(L);
     uint32_t ray_head = 0, hit_tail = 0, hit_head = 0;   // hit_head: last value seen (the shading wave owns it)
     uint64_t maps = 0, iters = 0;
     const int T = P.shade_threshold, TR = P.refill_threshold;
