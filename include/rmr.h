@@ -177,13 +177,14 @@ int rmr_set_env_map(rmr_ctx* ctx, const uint8_t* rgba8, int w, int h);
  * (GL_NEAREST, Graphics.h:90-91), alpha 1 inside [min, max] and 0 elsewhere, GL_FRAMEBUFFER_SRGB
  * encode (byte = round(255 srgb(clamp(c, 0, 1))), exact; rmr_srgb_thresholds) and the
  * SRC_ALPHA / ONE_MINUS_SRC_ALPHA blend: pixels drawn with alpha 1 are replaced, every other pixel
- * keeps the caller's content (the GUI behind the image). rgba8 is a host buffer (in/out). */
+ * keeps the caller's content (the GUI behind the image). rgba8 is a host buffer (in/out) of nbytes
+ * bytes; RMR_E_INVALID unless nbytes >= screen_w * screen_h * 4. */
 int rmr_display(rmr_ctx* ctx, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
-                float max_y, int screen_w, int screen_h, uint8_t* rgba8);
-/* The same into a device buffer (e.g. a torch uint8 tensor or an interop surface), on the context's
- * stream, without host copies or a sync. */
+                float max_y, int screen_w, int screen_h, uint8_t* rgba8, size_t nbytes);
+/* The same into a device buffer of nbytes bytes (e.g. a torch uint8 tensor or an interop surface), on
+ * the context's stream, without host copies or a sync. */
 int rmr_display_device(rmr_ctx* ctx, float centre_x, float centre_y, float zoom, float min_x, float min_y,
-                       float max_x, float max_y, int screen_w, int screen_h, void* rgba8_dev);
+                       float max_x, float max_y, int screen_w, int screen_h, void* rgba8_dev, size_t nbytes);
 /* The 256 sRGB decision points rmr_display uses: out[k] = the smallest float c with byte(c) >= k. */
 int rmr_srgb_thresholds(float out[256]);
 /* Test hook, no GPU needed: the candidate grid a context builds for a BVH scene's nearest-primitive

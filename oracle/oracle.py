@@ -24,27 +24,41 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = C.CDLL(LIB_PATH)
-        fp = C.POINTER(C.c_float)
-        L.oracle_sample.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, fp, C.POINTER(C.c_uint64)]
-        L.oracle_render.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32,
-                                    C.c_uint32, fp, C.c_int, C.POINTER(C.c_uint64)]
-        L.oracle_trace_samples.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32,
-                                           fp, C.c_int, C.POINTER(C.c_uint64)]
-        for n in ["oracle_det_sin", "oracle_det_cos", "oracle_det_acos", "oracle_det_log", "oracle_det_exp"]:
-            getattr(L, n).argtypes = [C.c_float]
-            getattr(L, n).restype = C.c_float
-        L.oracle_det_atan2.argtypes = [C.c_float, C.c_float]
-        L.oracle_det_atan2.restype = C.c_float
-        L.oracle_map.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
-        L.oracle_march.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Params), fp, fp, C.c_float, fp]
-        L.oracle_trace.argtypes = [C.POINTER(Job), C.c_int, C.c_int, C.c_float, fp, fp, fp]
-        L.oracle_normal.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
-        L.oracle_rand_chain.argtypes = [C.c_int, C.c_int, C.c_float, fp, C.c_int, fp]
-        L.oracle_hemisphere.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, fp, fp, fp, fp]
-        L.oracle_wl2rgb.argtypes = [C.c_uint32, fp]
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
+
+
+def literal_lib():
+    """The oracle built with the reference's literal expressions where the default build
+    reformulates them (RMR_HEMI_ALGEBRAIC=0: randHemisphere through acos / sin / cos as RM1:270-304;
+    RMR_MB_POLY=0: the power-8 Mandelbulb through angle doubling): oracle/_lit/liboracle_lit.so."""
+    path = os.path.join(HERE, "_lit", "liboracle_lit.so")
+    subprocess.check_call(["make", "-s", "-C", HERE, "lit"])
+    return load(path)
+
+
+def load(path):
+    """dlopen one build of the oracle and declare its entry points."""
+    L = C.CDLL(path)
+    fp = C.POINTER(C.c_float)
+    L.oracle_sample.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, fp, C.POINTER(C.c_uint64)]
+    L.oracle_render.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                C.c_uint32, fp, C.c_int, C.POINTER(C.c_uint64)]
+    L.oracle_trace_samples.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                       fp, C.c_int, C.POINTER(C.c_uint64)]
+    for n in ["oracle_det_sin", "oracle_det_cos", "oracle_det_acos", "oracle_det_log", "oracle_det_exp"]:
+        getattr(L, n).argtypes = [C.c_float]
+        getattr(L, n).restype = C.c_float
+    L.oracle_det_atan2.argtypes = [C.c_float, C.c_float]
+    L.oracle_det_atan2.restype = C.c_float
+    L.oracle_map.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
+    L.oracle_march.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Params), fp, fp, C.c_float, fp]
+    L.oracle_trace.argtypes = [C.POINTER(Job), C.c_int, C.c_int, C.c_float, fp, fp, fp]
+    L.oracle_normal.argtypes = [C.POINTER(abi.Scene), C.c_float, fp, fp]
+    L.oracle_rand_chain.argtypes = [C.c_int, C.c_int, C.c_float, fp, C.c_int, fp]
+    L.oracle_hemisphere.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, fp, fp, fp, fp]
+    L.oracle_wl2rgb.argtypes = [C.c_uint32, fp]
+    return L
 
 
 def _fp(a):
@@ -117,11 +131,11 @@ def det(name, *args):
     return getattr(lib(), "oracle_det_" + name)(*[C.c_float(a) for a in args])
 
 
-def map_p(tables, p, max_dist=1000.0):
+def map_p(tables, p, max_dist=1000.0, L=None):
     s = tables.to_ctypes()
     P = np.asarray(p, np.float32)
     out = np.zeros(2, np.float32)
-    lib().oracle_map(C.byref(s), max_dist, _fp(P), _fp(out))
+    (L or lib()).oracle_map(C.byref(s), max_dist, _fp(P), _fp(out))
     return out
 
 
@@ -148,9 +162,9 @@ def rand_chain(gx, gy, time, cos):
     return out
 
 
-def hemisphere(gx, gy, time, rc0, s1, s2, n):
+def hemisphere(gx, gy, time, rc0, s1, s2, n, L=None):
     out = np.zeros(3, np.float32)
-    lib().oracle_hemisphere(gx, gy, time, rc0, _fp(np.asarray(s1, np.float32)), _fp(np.asarray(s2, np.float32)),
+    (L or lib()).oracle_hemisphere(gx, gy, time, rc0, _fp(np.asarray(s1, np.float32)), _fp(np.asarray(s2, np.float32)),
                             _fp(np.asarray(n, np.float32)), _fp(out))
     return out
 

@@ -100,8 +100,8 @@ def lib():
         "rmr_scene_compile": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "rmr_scene_view": (C.c_int, [vp, C.POINTER(abi.Scene)]),
         "rmr_scene_free": (None, [vp]),
-        "rmr_display": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
-        "rmr_display_device": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p]),
+        "rmr_display": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
+        "rmr_display_device": (C.c_int, [vp] + [C.c_float] * 7 + [C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
         "rmr_srgb_thresholds": (C.c_int, [fp]),
         "rmr_candidate_grid": (C.c_int, [fp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                          C.POINTER(C.c_int32), fp, C.POINTER(C.c_uint32), C.c_size_t,

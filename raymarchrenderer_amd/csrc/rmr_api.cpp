@@ -1237,9 +1237,11 @@ int display_common(rmr_ctx* c, float cx, float cy, float zoom, float min_x, floa
 }  // namespace
 
 int rmr_display(rmr_ctx* c, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
-                float max_y, int screen_w, int screen_h, uint8_t* rgba8) {
+                float max_y, int screen_w, int screen_h, uint8_t* rgba8, size_t nbytes) {
     if (!c || !rgba8 || screen_w <= 0 || screen_h <= 0 || screen_w > 32768 || screen_h > 32768)
         return fail(c, RMR_E_INVALID, "rmr_display: bad screen image");
+    if (nbytes < (size_t)screen_w * screen_h * 4)
+        return fail(c, RMR_E_INVALID, "rmr_display: screen buffer smaller than screen_w * screen_h * 4 bytes");
     HIPCHK(c, hipSetDevice(c->device));
     const size_t n = (size_t)screen_w * screen_h;
     if (n > c->screen_cap) {
@@ -1259,9 +1261,11 @@ int rmr_display(rmr_ctx* c, float centre_x, float centre_y, float zoom, float mi
 }
 
 int rmr_display_device(rmr_ctx* c, float centre_x, float centre_y, float zoom, float min_x, float min_y, float max_x,
-                       float max_y, int screen_w, int screen_h, void* rgba8_dev) {
+                       float max_y, int screen_w, int screen_h, void* rgba8_dev, size_t nbytes) {
     if (!c || !rgba8_dev || screen_w <= 0 || screen_h <= 0 || screen_w > 32768 || screen_h > 32768)
         return fail(c, RMR_E_INVALID, "rmr_display_device: bad screen image");
+    if (nbytes < (size_t)screen_w * screen_h * 4)
+        return fail(c, RMR_E_INVALID, "rmr_display_device: screen buffer smaller than screen_w * screen_h * 4 bytes");
     HIPCHK(c, hipSetDevice(c->device));
     return display_common(c, centre_x, centre_y, zoom, min_x, min_y, max_x, max_y, screen_w, screen_h,
                           (uint32_t*)rgba8_dev);

@@ -243,17 +243,22 @@ class Renderer:
             w, h = screen_size
             screen = np.zeros((int(h), int(w), 4), np.uint8)
         screen = np.ascontiguousarray(screen, np.uint8)
+        if screen.ndim != 3 or screen.shape[2] != 4:
+            raise ValueError("display: screen must be an (h, w, 4) RGBA8 image, got shape %s" % (screen.shape,))
         h, w = screen.shape[:2]
         _check(self._ctx, lib().rmr_display(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
                                             float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
-                                            w, h, screen.ctypes.data))
+                                            w, h, screen.ctypes.data, screen.nbytes))
         return screen
 
-    def display_device(self, centre, zoom, vmin, vmax, dev_ptr, screen_w, screen_h):
-        """rmr_display_device: the same into a device RGBA8 buffer on the renderer's stream."""
+    def display_device(self, centre, zoom, vmin, vmax, dev_ptr, screen_w, screen_h, nbytes=None):
+        """rmr_display_device: the same into a device RGBA8 buffer of `nbytes` bytes (default
+        screen_w * screen_h * 4) on the renderer's stream."""
+        if nbytes is None:
+            nbytes = int(screen_w) * int(screen_h) * 4
         _check(self._ctx, lib().rmr_display_device(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
                                                    float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
-                                                   int(screen_w), int(screen_h), C.c_void_p(dev_ptr)))
+                                                   int(screen_w), int(screen_h), C.c_void_p(dev_ptr), int(nbytes)))
 
     def stats(self):
         s = abi.Stats()

@@ -77,3 +77,25 @@ def test_display_device_buffer_matches_host_path():
         assert np.array_equal(dev.cpu().numpy(), host)
     finally:
         r.close()
+
+
+@pytest.mark.gpu
+def test_display_rejects_wrong_screen_buffers():
+    """A screen that is not (h, w, 4) RGBA8 is refused before any copy (renderer.py), and the C ABI
+    refuses a buffer smaller than screen_w * screen_h * 4 bytes (rmr_display / rmr_display_device)."""
+    import ctypes as C
+    from raymarchrenderer_amd import RMRError, Renderer, abi
+    from raymarchrenderer_amd._lib import lib
+    r = Renderer(0, 16, 16)
+    try:
+        with pytest.raises(ValueError):
+            r.display((8.0, 8.0), 1.0, (0, 0), (16, 16), screen=np.zeros((16, 16, 3), np.uint8))
+        buf = np.zeros((16, 16, 4), np.uint8)
+        rc = lib().rmr_display(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, buf.ctypes.data, buf.nbytes - 1)
+        assert rc == abi.RMR_E_INVALID
+        rc = lib().rmr_display_device(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, C.c_void_p(1), 16 * 16 * 4 - 4)
+        assert rc == abi.RMR_E_INVALID
+        with pytest.raises(RMRError):
+            r.display_device((8.0, 8.0), 1.0, (0, 0), (16, 16), 1, 16, 16, nbytes=100)
+    finally:
+        r.close()

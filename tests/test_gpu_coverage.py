@@ -5,8 +5,9 @@
   schedule time(f, s) = 1000 f + 0.016 s, bitwise against the oracle at frames 1, 37 and 90;
 * sample-plane chunking (rmr_api.cpp render_tiles: launches split at the sample-plane budget) —
   several launches per frame fold to the same bits as one;
-* the full C2 frame (1920x1080) through the multi-GPU tile path, checked by properties that do not
-  depend on size (finite, non-negative, alpha 1) and bitwise against the oracle on random 8x8 tiles;
+* the full C2, C3, C4 and C5 frames (1920x1080; C4 3840x2160) through the multi-GPU tile path,
+  checked by properties that do not depend on size (finite, non-negative, alpha 1) and bitwise
+  against the oracle on random 8x8 tiles;
 * FrameRenderer's stream ordering (zero -> render -> collective on one stream) read back on that
   stream only, and rmr_render_tiles' rejection of repeated tiles.
 """
@@ -126,6 +127,70 @@ def test_full_c2_frame_properties_and_sampled_tiles(renderer):
         cpu = orc.render(times, rect=(x0, y0, x0 + 8, y0 + 8))
         eq = _same(img[y0:y0 + 8, x0:x0 + 8], cpu[y0:y0 + 8, x0:x0 + 8])
         assert eq.all(), "tile (%d, %d)" % (x0, y0)
+
+
+def _full_frame_check(renderer, scene, W, H, spp, bounces, frame=0, ntiles=6, seed=11,
+                      mean_range=(0.0, 10.0)):
+    """Render a BASELINE config's full frame through rmr_render_tiles (32x32 tiles, the bench's
+    path: the specialised kernel rmr_jit_trace), then check size-independent properties (finite,
+    non-negative, alpha 1, a plausible frame mean) and `ntiles` random 8x8 tiles bitwise against
+    the oracle (RM1:567-613 per pixel)."""
+    from raymarchrenderer_amd.multi_gpu import frame_tiles
+    prm, view = _setup(renderer, scene, W, H, max_bounces=bounces)
+    times = time_schedule(spp, frame=frame)
+    renderer.reset_stats()
+    renderer.render_tiles(times, frame_tiles(W, H, 32), 32)
+    img = renderer.read_accum()
+    st = renderer.stats()
+    assert st.jit_launches == st.trace_launches >= 1
+    assert np.isfinite(img).all()
+    assert (img[..., :3] >= 0).all() and (img[..., 3] == 1.0).all()
+    m = float(img[..., :3].mean())
+    assert mean_range[0] < m < mean_range[1], m
+    tables = scene_compile.compile_scene(scene, "rm1") if isinstance(scene, dict) else \
+        scene_compile.load_scene_file(scene, "rm1")
+    orc = oracle.Oracle(tables, prm, view, W, H)
+    rng = np.random.default_rng(seed)
+    picks = [(int(rng.integers(0, W // 8)) * 8, int(rng.integers(0, H // 8)) * 8) for _ in range(ntiles)]
+    # plus two of the busiest tiles (largest radiance spread: edges, the primitives' cluster), which
+    # uniform picks can miss on a mostly-empty frame
+    lum = img[: H // 8 * 8, : W // 8 * 8, :3].sum(-1).reshape(H // 8, 8, W // 8, 8)
+    spread = lum.std(axis=(1, 3)).ravel()
+    top = np.argsort(spread)[-max(1, spread.size // 100):]
+    for k in rng.choice(top, 2, replace=False):
+        picks.append((int(k % (W // 8)) * 8, int(k // (W // 8)) * 8))
+    for x0, y0 in picks:
+        cpu = orc.render(times, rect=(x0, y0, x0 + 8, y0 + 8))
+        eq = _same(img[y0:y0 + 8, x0:x0 + 8], cpu[y0:y0 + 8, x0:x0 + 8])
+        assert eq.all(), "tile (%d, %d): %d values differ" % (x0, y0, (~eq).sum())
+    return img, st
+
+
+def test_full_c3_frame_properties_and_sampled_tiles(renderer):
+    """C3 (BASELINE configs[2]): the Mandelbulb at its production size 1920x1080, 2 bounces;
+    2 spp instead of 128 (the sample loop is the same code at every spp)."""
+    _full_frame_check(renderer, os.path.join(SCENES, "mandelbulb.scene"), 1920, 1080, 2, 2,
+                      ntiles=8, seed=31, mean_range=(0.005, 1.0))
+
+
+def test_full_c4_frame_properties_and_sampled_tiles(renderer):
+    """C4 (BASELINE configs[3]): the 256-primitive union at its production size 3840x2160,
+    4 bounces, through the nearest-primitive cache and the candidate grid; 1 spp instead of 256.
+    The tiles include ones on the sphere cluster (the grid's region)."""
+    img, st = _full_frame_check(renderer, os.path.join(SCENES, "csg256.scene"), 3840, 2160, 1, 4,
+                                ntiles=8, seed=41, mean_range=(0.005, 2.0))
+    assert st.map_evals > 0
+
+
+def test_full_c5_frame_properties_and_sampled_tiles(renderer):
+    """C5 (BASELINE configs[4]): an animated frame (f = 37, the sphere moved: the live-primitive
+    kernel) at 1920x1080, 4 bounces, on the bench's large-seed schedule; 2 spp instead of 512.
+    Frame 0 first, so that the layout's kernel is baked and frame 37 switches it to live."""
+    from raymarchrenderer_amd.multi_gpu import frame_tiles
+    _setup(renderer, _c5_scene(0), 1920, 1080, max_bounces=4)
+    renderer.render_tiles(time_schedule(1, frame=0), frame_tiles(1920, 1080, 32), 32)
+    _full_frame_check(renderer, _c5_scene(37), 1920, 1080, 2, 4, frame=37, ntiles=6, seed=53,
+                      mean_range=(0.05, 1.0))
 
 
 def test_frame_renderer_stream_ordering_without_device_sync():

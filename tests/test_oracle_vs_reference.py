@@ -114,6 +114,111 @@ def test_kat_rand_and_hemisphere_distributions(name):
     assert (np.sum(ours_h * nrm, axis=1) >= -1e-6).all()
 
 
+def _ks_uniform(x):
+    """One-sample Kolmogorov-Smirnov statistic of x against U[0, 1]."""
+    x = np.sort(np.asarray(x, np.float64))
+    n = len(x)
+    i = np.arange(1, n + 1)
+    return max(np.max(i / n - x), np.max(x - (i - 1) / n))
+
+
+def _hemi_polar(h, n):
+    """cos(theta) about the normal and the azimuth / 2pi in a tangent frame fixed by the normal.
+    A uniform hemisphere (RM1:270-304) makes both U[0, 1]; a cosine-weighted one makes cos(theta)
+    ~ sqrt(U) (KS distance 0.25)."""
+    h = np.asarray(h, np.float64)
+    n = np.asarray(n, np.float64)
+    n = n / np.linalg.norm(n, axis=1, keepdims=True)
+    a = np.where(np.abs(n[:, 1:2]) > 0.9, [[1.0, 0.0, 0.0]], [[0.0, 1.0, 0.0]])
+    t = np.cross(n, a)
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    b = np.cross(n, t)
+    ct = np.sum(h * n, axis=1)
+    phi = np.arctan2(np.sum(h * b, axis=1), np.sum(h * t, axis=1))
+    return np.clip(ct, 0.0, 1.0), (phi / (2.0 * np.pi)) % 1.0
+
+
+def _hemi_kats():
+    ins, outs = [], []
+    for name in sorted(KATS):
+        k = np.load(os.path.join(GOLDEN, "kat_%s.npz" % name))
+        ins.append((k["hemi_in"], float(k["rand_time"]), int(k["probe_width"])))
+        outs.append(k["hemi_out"])
+    return ins, outs
+
+
+def test_hemisphere_distribution_ks_vs_reference():
+    """randHemisphere (RM1:270-304) as a distribution: the reference's own samples (llvmpipe,
+    3072 pooled over the KAT scenes) and the oracle's on the same inputs are each uniform on the
+    hemisphere by KS (cos(theta) and the azimuth; critical distance at alpha = 0.001 is 1.95/sqrt(n)),
+    and the two samples agree by a two-sample KS. A cosine-weighted or a tilted sampler fails."""
+    ins, outs = _hemi_kats()
+    ref_h = np.concatenate(outs)
+    nrm = np.concatenate([i[0][:, 4:7] for i in ins])
+    ours = np.concatenate([
+        np.array([oracle.hemisphere(j % w, j // w, t, r[8], r[0:2], r[2:4], r[4:7]) for j, r in enumerate(hin)])
+        for hin, t, w in ins])
+    n = len(ref_h)
+    crit = 1.95 / np.sqrt(n)
+    polar = {}
+    for label, h in (("reference", ref_h), ("oracle", ours)):
+        ct, ph = _hemi_polar(h, nrm)
+        polar[label] = (ct, ph)
+        assert _ks_uniform(ct) < crit, (label, "cos theta", _ks_uniform(ct))
+        assert _ks_uniform(ph) < crit, (label, "azimuth", _ks_uniform(ph))
+        # a cosine-weighted sampler (cos theta = sqrt(u)) would be far outside
+        assert _ks_uniform(np.sqrt(np.linspace(0, 1, n))) > 4 * crit
+    # two-sample KS between reference and oracle: critical 1.95 sqrt(2/n)
+    for j in range(2):
+        a, b = np.sort(polar["reference"][j]), np.sort(polar["oracle"][j])
+        grid = np.concatenate([a, b])
+        d = np.max(np.abs(np.searchsorted(a, grid, "right") / n - np.searchsorted(b, grid, "right") / n))
+        assert d < 1.95 * np.sqrt(2.0 / n), (j, d)
+
+
+def test_hemisphere_algebraic_form_vs_literal_within_ulps():
+    """The default oracle (and kernel) takes cos(acos(u)) = u and sin(acos(u)) = sqrt(1 - u^2)
+    algebraically; the literal build (RMR_HEMI_ALGEBRAIC=0) evaluates RM1:270-304's acos / sin / cos.
+    On every KAT input the two directions agree within a few float ulps of a unit vector.
+
+    One exception, and it is the reference's own driver-defined edge: when rand() returns exactly 0,
+    u = -1 and the direction lies in the tangent plane; sin(acos(-1)) is sin(float(pi)) = -8.7e-8 in
+    the literal form (the driver's sign, GLSL does not fix it) and +0 algebraically, so RM1:287's
+    `if (b.z < 0) b = -b` flips one and not the other. Both are the same grazing direction up to the
+    flip (4 of the 3072 KAT inputs)."""
+    lit = oracle.literal_lib()
+    ins, _ = _hemi_kats()
+    worst, flips = 0.0, 0
+    for hin, t, w in ins:
+        for j, r in enumerate(hin):
+            a = oracle.hemisphere(j % w, j // w, t, r[8], r[0:2], r[2:4], r[4:7])
+            b = oracle.hemisphere(j % w, j // w, t, r[8], r[0:2], r[2:4], r[4:7], L=lit)
+            d = float(np.abs(a - b).max())
+            if d > 8 * 2.0 ** -23 and abs(float(np.dot(a, r[4:7]))) < 1e-6 and np.abs(a + b).max() <= 8 * 2.0 ** -23:
+                flips += 1
+                continue
+            worst = max(worst, d)
+    assert worst <= 8 * 2.0 ** -23, worst   # <= 8 ulps of 1.0 per component
+    assert flips <= 8, flips
+
+
+def test_mandelbulb_poly_vs_literal_within_map_rtol():
+    """The power-8 Mandelbulb as complex powers (mb_iter8_poly, default) against the angle-doubling
+    form (RMR_MB_POLY=0), both transcendental-free restatements of the trigonometric iteration:
+    the distance estimates on the KAT points agree within MAP_RTOL, the tolerance the oracle is held
+    to against the reference GLSL's own trigonometric iteration on llvmpipe."""
+    lit = oracle.literal_lib()
+    k = np.load(os.path.join(GOLDEN, "kat_mandelbulb.npz"))
+    t = _tables(*KATS["mandelbulb"])
+    a = np.array([oracle.map_p(t, p) for p in k["map_in"]])
+    b = np.array([oracle.map_p(t, p, L=lit) for p in k["map_in"]])
+    assert np.all(np.abs(a[:, 0] - b[:, 0]) <= MAP_RTOL["mandelbulb"] * np.maximum(1.0, np.abs(b[:, 0])))
+    assert np.array_equal(a[:, 1], b[:, 1])
+    # and the literal build is itself within the same tolerance of the reference
+    ref = k["map_out"]
+    assert np.all(np.abs(b[:, 0] - ref[:, 0]) <= MAP_RTOL["mandelbulb"] * np.maximum(1.0, np.abs(ref[:, 0])))
+
+
 IMAGES = {
     "rm3_builtin": (None, "rm3", {}),
     "rm1_cornell5_b4": (os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 4}),
@@ -124,6 +229,10 @@ IMAGES = {
     "rm1_default": (os.path.join(GOLDEN, "scenes", "default.scene"), "rm1", {}),
     "rm1_sphere1_env": (os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}),
     "rm2_simple_env": (os.path.join(GOLDEN, "scenes", "simple.scene"), "rm2", {"use_env_tex": 1}),
+    # round-2 goldens: C4's generator cut to 64 primitives, RM1's object node set, C3's Mandelbulb
+    "rm1_csg64_b4": (os.path.join(SCENES, "csg64.scene"), "rm1", {"max_bounces": 4}),
+    "rm1_csg_nodes_b4": (os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}),
+    "rm1_mandelbulb_b2": (os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}),
 }
 
 

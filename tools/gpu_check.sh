@@ -3,7 +3,7 @@
 # (exit 124/134/137/139); a plain test failure (exit 1) still lets the bench run.
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
-timeout -k 10 ${T_TEST:-420} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${T_TEST:-420} python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --durations=20 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
