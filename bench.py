@@ -12,6 +12,9 @@ The other BASELINE configs run with --config (they are separate bench lines, not
   c4  256-prim union (scenes/csg256.scene) 3840x2160, 256 spp, 4 bounces
   c5  animated Cornell-5, 1920x1080, 512 spp, 4 bounces: step f renders frame f (sphere centre
       y = 0.5 sin(2 pi f / 120)); the scene is recompiled and uploaded inside the timed step
+  rm3 RayMarch3.glsl as the reference wires it (Graphics.cpp:272): built-in spectral scene,
+      1920x1080, 4 spp, 16 bounces (the reference's own CPU path measured 5.2-5.4 Msamples/s)
+  rm2 RayMarch2.glsl (NEE) on simple.scene, 1920x1080, 4 spp, 16 bounces (llvmpipe 18-20)
 
 Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL). `--gpus N` without a
 launcher's WORLD_SIZE starts N rank processes itself (before anything in the parent touches the
@@ -53,7 +56,35 @@ CONFIGS = {
     "c4": dict(scene="csg256.scene", W=3840, H=2160, spp=256, bounces=4, name="C4 256-prim CSG union"),
     "c5": dict(scene="cornell5.scene", W=1920, H=1080, spp=512, bounces=4, name="C5 animated Cornell-5",
                animated=True),
+    # the reference's own kernels where its CPU path was measured: RayMarch3.glsl as
+    # Graphics.cpp:272 wires it (3-primitive spectral scene, maxBounces 16) and the RM2 NEE variant on
+    # simple.scene; 1920x1080, 4 spp, as measured on llvmpipe
+    "rm3": dict(scene=None, variant="rm3", W=1920, H=1080, spp=4, bounces=16,
+                name="RM3 as wired (RayMarch3.glsl built-in scene)"),
+    "rm2": dict(scene="../tests/golden/scenes/simple.scene", variant="rm2", W=1920, H=1080, spp=4, bounces=16,
+                name="RM2 simple.scene (RayMarch2.glsl NEE)"),
 }
+
+
+def variant_of(cfg):
+    return cfg.get("variant", "rm1")
+
+
+def load_into(r, cfg, scene):
+    """Load a config's scene (path or dict; None = the variant's built-in scene) into a Renderer."""
+    if scene is None:
+        r.load_builtin(variant_of(cfg))
+    else:
+        r.load_scene(scene, variant_of(cfg))
+
+
+def oracle_tables(cfg, scene):
+    from oracle import scene_compile
+    if scene is None:
+        return scene_compile.compile_scene({}, variant_of(cfg))
+    if isinstance(scene, str):
+        return scene_compile.load_scene_file(scene, variant_of(cfg))
+    return scene_compile.compile_scene(scene, variant_of(cfg))
 
 
 def parse():
@@ -81,6 +112,11 @@ def parse():
                     help="GPU rehearsal of the multi-rank path on a one-GPU box: every rank renders on "
                          "cuda:0 with the HIP kernels, the frame reduce runs over gloo (staged through "
                          "host memory); a correctness rehearsal, not a scaling measurement")
+    ap.add_argument("--predict", default="",
+                    help="comma-separated rank counts (e.g. 2,4,8): on ONE GPU, time each rank's tile share of the "
+                         "frame in turn (two overlapping contexts, as at N > 1) for 32x32 and 64x64 tiles, and the "
+                         "sample-split alternative; prints the per-rank times, the imbalance and the predicted "
+                         "speed-up (SURVEY §8e)")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip rank 0's check of the last reduced frame against a one-context render")
     return ap.parse_args()
@@ -89,7 +125,9 @@ def parse():
 def scene_for_frame(cfg, frame):
     """Scene dict for a frame: static configs return the file; C5 moves the Cornell sphere
     (objects[3]) to y = 0.5 sin(2 pi f / 120)."""
-    path = os.path.join(ROOT, "scenes", cfg["scene"])
+    if cfg["scene"] is None:
+        return None
+    path = os.path.normpath(os.path.join(ROOT, "scenes", cfg["scene"]))
     if not cfg.get("animated"):
         return path
     with open(path) as f:
@@ -98,34 +136,66 @@ def scene_for_frame(cfg, frame):
     return sc
 
 
-def cpu_baseline(cfg, spp, seconds, threads):
+def cpu_threads():
+    """Threads for the CPU leg: every CPU this process may run on (its affinity set), capped by
+    OMP_NUM_THREADS where the environment sets it. On the GPU box the harness sets 16, the host-CPU
+    share of one GPU (the machine's other CPUs belong to other GPUs' jobs); in this container 8."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
+
+
+def cpu_baseline(cfg, spp, seconds, threads, repeats=3):
     """CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload: 40 rows
-    spread over the frame, samples 0.. of the same schedule, repeated until ~`seconds` pass."""
-    from oracle import camera, oracle, scene_compile
+    spread over the frame, samples 0.. of the same schedule. `repeats` timed runs of ~seconds/repeats
+    each after one untimed warm-up row pass; the median is reported."""
+    import statistics
+    from oracle import camera, oracle
     from raymarchrenderer_amd import abi, time_schedule
     W, H = cfg["W"], cfg["H"]
-    sc = scene_for_frame(cfg, 0)
-    t = scene_compile.load_scene_file(sc, "rm1") if isinstance(sc, str) else scene_compile.compile_scene(sc, "rm1")
-    o = oracle.Oracle(t, abi.default_params(max_bounces=cfg["bounces"]), camera.default_view(W, H), W, H)
+    o = oracle.Oracle(oracle_tables(cfg, scene_for_frame(cfg, 0)), abi.default_params(max_bounces=cfg["bounces"]),
+                      camera.default_view(W, H), W, H)
     stride = max(1, H // 40)
     rows = list(range(0, H, stride))
+    # rows in bit-reversed order (any prefix is spread over the frame), each with the schedule's first
+    # min(spp, 4) samples; every repeat renders the same prefix of this list again, so the repeats
+    # time identical work and the median is a plain timing median
+    nb = max(1, (len(rows) - 1).bit_length())
+    order = sorted(range(len(rows)), key=lambda i: int(format(i, "0%db" % nb)[::-1], 2))
+    ns = min(spp, 4)
+    units = [(rows[i], s) for i in order for s in range(ns)]
     times = time_schedule(spp)
-    done = 0
-    t0 = time.perf_counter()
-    k = 0
-    while True:
-        y = rows[k % len(rows)]
-        s = (k // len(rows)) % spp
+    # untimed warm-up (~1/8 of the budget): the OpenMP pool and the cores' clocks settle (measured: the
+    # first second of RM3 rows ran up to 10x slower than the same rows afterwards)
+    t0, i = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds / 8:
+        y, s = units[i % len(units)]
         o.render(times[s:s + 1], rect=(0, y, W, y + 1), first_sample=s, nthreads=threads)
-        done += W
-        k += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    out = {"value": done / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": "%d samples: rows y%%%d==0 of the %dx%d frame, 1 spp per row pass, %d-thread OpenMP C "
-                     "restatement (oracle/rmr_oracle.c); %d threads = the host-CPU share of one GPU on "
-                     "this box (OMP_NUM_THREADS)" % (done, stride, W, H, threads, threads)}
+        i += 1
+    rates, total = [], 0
+    for _ in range(repeats):
+        done = 0
+        i = 0
+        t0 = time.perf_counter()
+        while True:
+            y, s = units[i % len(units)]
+            o.render(times[s:s + 1], rect=(0, y, W, y + 1), first_sample=s, nthreads=threads)
+            done += W
+            i += 1
+            if time.perf_counter() - t0 >= seconds / repeats:
+                break
+        rates.append(done / (time.perf_counter() - t0) / 1e6)
+        total += done
+    out = {"value": statistics.median(rates), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "repeats_msamples_per_s": [round(x, 4) for x in rates],
+           "sample": "median of %d timed runs (%d samples in all) of the same work: rows y%%%d==0 of the %dx%d "
+                     "frame (bit-reversed order) x the schedule's first %d samples, %d-thread OpenMP C restatement (oracle/rmr_oracle.c); %d threads = every CPU "
+                     "of this process's affinity set, capped by OMP_NUM_THREADS (the host-CPU share of one GPU "
+                     "on the GPU box)" % (repeats, total, stride, W, H, ns, threads, threads),
+           "host_cpus_visible": os.cpu_count()}
     ref = LLVMPIPE_PER_VCPU.get(cfg_name_of(cfg))
     if ref:
         # the reference's own path (RayMarch.glsl on Mesa llvmpipe) cannot run on the GPU box (no
@@ -142,6 +212,8 @@ LLVMPIPE_PER_VCPU = {
     "c1": (3.65 / 8, "RM1 single sphere 256x256 1 spp: 3.5-3.8 Msamples/s on 8 vCPU"),
     "c2": (3.56 / 8, "RM1 Cornell-5 1920x1080 4 bounces: 3.56 Msamples/s on 8 vCPU"),
     "c5": (3.56 / 8, "RM1 Cornell-5 (C5's scene, static) 1920x1080 4 bounces: 3.56 Msamples/s on 8 vCPU"),
+    "rm3": (5.3 / 8, "RM3 as wired 1920x1080 4 spp 16 bounces: 5.2-5.4 Msamples/s on 8 vCPU"),
+    "rm2": (19.0 / 8, "RM2 simple.scene 1920x1080 4 spp 16 bounces: 18-20 Msamples/s on 8 vCPU"),
 }
 
 
@@ -157,7 +229,8 @@ def cfg_name_of(cfg):
 # C5's is the animation's frame 0 (the sphere at y = 0 is the static Cornell-5 scene)
 GOLDEN_OF = {"c1": ("img_rm1_sphere1_b1.npz", "sphere1.scene"), "c2": ("img_rm1_cornell5_b4.npz", "cornell5.scene"),
              "c3": ("img_rm1_mandelbulb_b2.npz", "mandelbulb.scene"), "c4": ("img_rm1_csg64_b4.npz", "csg64.scene"),
-             "c5": ("img_rm1_cornell5_b4.npz", "cornell5.scene")}
+             "c5": ("img_rm1_cornell5_b4.npz", "cornell5.scene"), "rm3": ("img_rm3_builtin.npz", None),
+             "rm2": ("img_rm2_simple.npz", "../tests/golden/scenes/simple.scene")}
 
 
 def psnr_vs_reference(cfg_name, cfg, device):
@@ -175,7 +248,7 @@ def psnr_vs_reference(cfg_name, cfg, device):
     n = int(g["spp_conv"])
     r = Renderer(device, W, H)
     try:
-        r.load_scene(os.path.join(ROOT, "scenes", scene), "rm1")
+        load_into(r, cfg, None if scene is None else os.path.normpath(os.path.join(ROOT, "scenes", scene)))
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
         r.set_view(g["view"])
         r.render_spp(parity_schedule(n))
@@ -187,7 +260,9 @@ def psnr_vs_reference(cfg_name, cfg, device):
     psnr = 10 * np.log10(1.0 / max(np.mean((a - b) ** 2), 1e-30))
     rel = (img[..., :3].mean() - ref[..., :3].mean()) / max(float(ref[..., :3].mean()), 1e-12)
     return {"psnr_db": round(float(psnr), 2), "mean_rel_diff": round(float(rel), 5),
-            "reference": "RayMarch.glsl on Mesa llvmpipe, %s, %dx%d, %d spp (tests/golden/%s)" % (scene, W, H, n, name),
+            "reference": "%s on Mesa llvmpipe, %s, %dx%d, %d spp (tests/golden/%s)"
+                         % ({"rm1": "RayMarch.glsl", "rm2": "RayMarch2.glsl", "rm3": "RayMarch3.glsl"}[variant_of(cfg)],
+                            os.path.basename(scene) if scene else "built-in scene", W, H, n, name),
             "gpu_spp": n}
 
 
@@ -208,7 +283,7 @@ def count_pass(cfg, spp, device, n_count=8):
     r = Renderer(device, W, H)
     try:
         r.set_jit(1)
-        r.load_scene(scene_for_frame(cfg, 0), "rm1")
+        load_into(r, cfg, scene_for_frame(cfg, 0))
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
         r.reset_stats()
         r.render_tiles(time_schedule(n), frame_tiles(W, H, TILE), TILE)
@@ -307,7 +382,7 @@ def verify_last_frame(cfg, fr, times, scene, spp, device):
     got = fr.last.cpu().numpy()
     r = Renderer(device, W, H)
     try:
-        r.load_scene(scene, "rm1")
+        load_into(r, cfg, scene)
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
         r.render_tiles(times, frame_tiles(W, H, TILE), TILE)
         want = r.read_accum()
@@ -338,8 +413,7 @@ def dry_run(args, cfg, rank, world):
     W, H, T = DRY_W, DRY_H, DRY_TILE
 
     def render_into(acc_np, tiles, times, sc):
-        t = scene_compile.load_scene_file(sc, "rm1") if isinstance(sc, str) else scene_compile.compile_scene(sc, "rm1")
-        o = oracle.Oracle(t, abi.default_params(max_bounces=cfg["bounces"]), camera.default_view(W, H), W, H)
+        o = oracle.Oracle(oracle_tables(cfg, sc), abi.default_params(max_bounces=cfg["bounces"]), camera.default_view(W, H), W, H)
         for tx, ty in tiles:
             o.render(times, rect=(tx * T, ty * T, min(W, (tx + 1) * T), min(H, (ty + 1) * T)), accum=acc_np,
                      nthreads=2)
@@ -374,6 +448,80 @@ def dry_run(args, cfg, rank, world):
     return 0 if ok else 1
 
 
+def predict_partition(args, cfg):
+    """One GPU stands in for N: rank k's share of the frame (FrameRenderer's round-robin tile subset
+    for rank k of N, no collective) is timed for k = 0..N-1 in turn, with two renderer contexts on two
+    streams as every rank runs at N > 1. The frame at N = 1 is timed the same way. Predicted speed-up
+    at N = T(1) / max_k T_k(N): the slowest rank sets the frame time (the reduce, ~0.3 ms per 1080p
+    frame over xGMI, is not included). Also the sample-split alternative (every rank all tiles,
+    spp / N samples): T(1) / T_split(N)."""
+    import torch
+    from raymarchrenderer_amd import Renderer, abi, time_schedule
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer
+    W, H = cfg["W"], cfg["H"]
+    spp = args.spp or cfg["spp"]
+    animated = bool(cfg.get("animated"))
+    rs, streams = [], []
+    for _ in range(2):
+        r = Renderer(0, W, H)
+        load_into(r, cfg, scene_for_frame(cfg, 0))
+        r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
+        r.set_jit(1)
+        s_ = torch.cuda.Stream()
+        r.set_stream(s_.cuda_stream)
+        rs.append(r)
+        streams.append(s_)
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+
+    def timed(tile, rank, world, nspp):
+        fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams)
+        f = [0]
+
+        def step():
+            if animated:
+                load_into(fr.next_renderer(), cfg, scene_for_frame(cfg, f[0] % 120))
+            fr.frame(time_schedule(nspp, frame=f[0] % 120 if animated else 0))
+            f[0] += 1
+        for _ in range(max(1, args.warmup)):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / args.steps * 1e3, len(fr.tiles)
+
+    out = {"config": args.config, "width": W, "height": H, "spp": spp, "steps": args.steps, "contexts": 2,
+           "one_gpu_ms": {}, "tiles": {}, "sample_split": {}}
+    ns = [int(x) for x in args.predict.split(",") if x.strip()]
+    for tile in (32, 64):
+        t1, _ = timed(tile, 0, 1, spp)
+        out["one_gpu_ms"][str(tile)] = round(t1, 3)
+        per_n = {}
+        for n in ns:
+            ms = [timed(tile, k, n, spp) for k in range(n)]
+            t = [m for m, _ in ms]
+            per_n[str(n)] = {"rank_ms": [round(x, 3) for x in t], "rank_tiles": [c for _, c in ms],
+                             "max_over_mean": round(max(t) / (sum(t) / len(t)), 4),
+                             "predicted_speedup": round(t1 / max(t), 3),
+                             "predicted_efficiency": round(t1 / max(t) / n, 3)}
+            print("predict tile %d N=%d: %s" % (tile, n, json.dumps(per_n[str(n)])), file=sys.stderr, flush=True)
+        out["tiles"][str(tile)] = per_n
+    t1 = out["one_gpu_ms"]["32"]
+    for n in ns:
+        if spp % n:
+            continue
+        ms, _ = timed(32, 0, 1, spp // n)
+        out["sample_split"][str(n)] = {"rank_ms": round(ms, 3), "predicted_speedup": round(t1 / ms, 3),
+                                       "note": "every rank renders every pixel with spp/N samples (not bitwise "
+                                               "the one-GPU running mean: a fallback, SURVEY §8e)"}
+    for r in rs:
+        r.close()
+    print(json.dumps({"partition_prediction": out}), flush=True)
+    return 0
+
+
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
@@ -386,6 +534,10 @@ def main():
         sys.exit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world))
     if args.dry_run:
         sys.exit(dry_run(args, cfg, rank, world))
+    if args.predict:
+        if world != 1:
+            sys.exit("bench.py --predict runs on one GPU (--gpus 1)")
+        sys.exit(predict_partition(args, cfg))
     W, H, BOUNCES = cfg["W"], cfg["H"], cfg["bounces"]
     spp = args.spp or cfg["spp"]
     import torch
@@ -413,7 +565,7 @@ def main():
     rs, streams = [], []
     for _ in range(n_ctx):
         r = Renderer(local_rank, W, H)
-        r.load_scene(scene_for_frame(cfg, 0), "rm1")
+        load_into(r, cfg, scene_for_frame(cfg, 0))
         r.set_params(abi.default_params(max_bounces=BOUNCES))
         if args.kernel:
             r.set_kernel(args.kernel)
@@ -446,7 +598,7 @@ def main():
         frame_no[0] += 1
         if animated:
             last["scene"], last["times"] = scene_for_frame(cfg, f % 120), time_schedule(spp, frame=f % 120)
-            fr.next_renderer().load_scene(last["scene"], "rm1")
+            load_into(fr.next_renderer(), cfg, last["scene"])
         else:
             last["scene"], last["times"] = scene_for_frame(cfg, 0), static_times
         fr.frame(last["times"])
@@ -550,8 +702,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(cfg, spp, args.cpu_seconds, threads)
+        cpu = cpu_baseline(cfg, spp, args.cpu_seconds, cpu_threads())
 
     parity = None
     if rank == 0 and not args.no_psnr:
@@ -562,8 +713,9 @@ def main():
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic",
-               "config": {"workload": "%s (RayMarch.glsl semantics) %dx%d %d spp %d bounces"
-                                      % (cfg["name"], W, H, spp, BOUNCES),
+               "config": {"workload": "%s (%s semantics) %dx%d %d spp %d bounces"
+                                      % (cfg["name"], {"rm1": "RayMarch.glsl", "rm2": "RayMarch2.glsl",
+                                                       "rm3": "RayMarch3.glsl"}[variant_of(cfg)], W, H, spp, BOUNCES),
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
                           "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world,
                           "frame_streams": n_ctx},

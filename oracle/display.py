@@ -3,8 +3,9 @@ createFQ 227-258, FullQuad.vs / FullQuad.fs) as rmr_display defines it headless;
 raymarchrenderer_amd's k_display (csrc/rmr_display.hip). Import only from tests/.
 
 Per screen pixel (row 0 = top), float32 arithmetic in the kernel's order:
-  h = (size / 2) * zoom; quad [c - h, c + h); fragment centre pos = pixel + 0.5 (rasterized if inside)
-  uv = (pos - (c - h)) / ((c + h) - (c - h)); texel = clamp(floor(uv * size))       (GL_NEAREST)
+  h = (size / 2) * zoom; quad x in [c - h, c + h), y in (c - h, c + h] (GL's tie rule, y flipped);
+  fragment centre pos = pixel + 0.5 (rasterized if inside)
+  uv = (pos - (c - h)) / ((c + h) - (c - h)); texel = floor(uv * size) mod size  (GL_NEAREST, GL_REPEAT)
   alpha 1 inside [min, max] (FullQuad.fs), else 0: alpha-1 pixels get sRGB8(texel.rgb), 255; every
   other pixel keeps the background (SRC_ALPHA / ONE_MINUS_SRC_ALPHA blend)
   sRGB8(c) = round(255 srgb(clamp(c, 0, 1))) exactly (GL_FRAMEBUFFER_SRGB), NaN -> 0
@@ -58,11 +59,14 @@ def display(accum, centre, zoom, vmin, vmax, screen):
     px = np.arange(sw, dtype=np.float32) + F(0.5)
     py = np.arange(sh, dtype=np.float32) + F(0.5)
     inx = (px >= x0) & (px < x1) & (px >= F(vmin[0])) & (px <= F(vmax[0]))
-    iny = (py >= y0) & (py < y1) & (py >= F(vmin[1])) & (py <= F(vmax[1]))
+    # GL's edge rule for a lower-left window origin (left / bottom edges in); FullQuad.vs flips y, so
+    # in screen rows the quad is (y0, y1] (measured on llvmpipe: tests/golden/display_*.npz)
+    iny = (py > y0) & (py <= y1) & (py >= F(vmin[1])) & (py <= F(vmax[1]))
     u = (px - x0) / (x1 - x0)
     v = (py - y0) / (y1 - y0)
-    i = np.clip(np.floor(u * F(W)), 0, W - 1).astype(np.int64)
-    j = np.clip(np.floor(v * F(H)), 0, H - 1).astype(np.int64)
+    # GL_NEAREST with GL_REPEAT (the default wrap; Framebuffer::Create sets only the filters)
+    i = np.mod(np.floor(u * F(W)).astype(np.int64), W)
+    j = np.mod(np.floor(v * F(H)).astype(np.int64), H)
     thr = srgb_thresholds()
     m = iny[:, None] & inx[None, :]
     tex = accum[j[:, None], i[None, :], :3]

@@ -7,6 +7,7 @@ Fixtures are data (inputs + reference outputs); the reference source itself is n
   kat_<scene>.npz   function-level known answers: map / march / getNormal / rand chain /
                     randHemisphere on fixed input sets (+ wavelengthToColor for RM3)
   img_<name>.npz    low-spp renders (4 spp) and converged renders (--conv-spp) of 64x48 images
+  display_ref.npz   Graphics::Display (FullQuad.vs / .fs, GL_FRAMEBUFFER_SRGB, blend) drawn screens
 MANIFEST.json records every configuration, the camera, the seed schedule and the GL driver.
 """
 import argparse
@@ -156,6 +157,44 @@ def make_image(name, path, variant, kw, conv_spp, threads):
     return dt
 
 
+# Graphics::Display cases on a 96x72 accumulator: centre, zoom, bounds min / max, screen (w, h)
+DISPLAY_CASES = [
+    ((64.0, 48.0), 1.0, (0, 0), (128, 96), (128, 96)),              # 1:1, texel centres on pixel centres
+    ((64.0, 48.0), 0.5, (1, 1), (127, 95), (128, 96)),              # the GUI's start zoom (GUI.cpp:187)
+    ((50.3, 40.9), 2.7, (20.5, 10.0), (110.0, 80.25), (128, 96)),   # magnified, clipped by the bounds
+    ((-20.0, 130.0), 1.3, (0, 0), (500, 500), (128, 96)),           # quad partly off screen
+    ((64.0, 48.0), 0.37, (0, 0), (1000, 1000), (131, 97)),          # minified, ragged screen
+    ((64.5, 48.5), 1.0, (0, 0), (500, 500), (128, 96)),             # quad edges through pixel centres
+    ((65.0, 49.0), 1.0, (10.5, 5.5), (100.5, 70.5), (128, 96)),     # bounds through pixel centres
+    ((60.25, 45.75), 3.0, (0, 0), (500, 500), (128, 96)),
+    ((64.0, 48.0), 0.25, (0, 0), (500, 500), (128, 96)),
+]
+
+
+def display_background(w, h):
+    """The screen content behind the quad (the GUI): a fixed pattern, alpha 7."""
+    y, x = np.mgrid[0:h, 0:w]
+    bg = np.stack([(7 * x + 13 * y) % 256, (11 * x + 3 * y + 50) % 256, (5 * x + 17 * y + 99) % 256,
+                   np.full_like(x, 7)], -1)
+    return bg.astype(np.uint8)
+
+
+def make_display():
+    """Graphics::Display (Graphics.cpp:356-390, FullQuad.vs / .fs) on llvmpipe over DISPLAY_CASES:
+    tests/golden/display_ref.npz holds the accumulator and every case's drawn screen."""
+    rng = np.random.default_rng(2024)
+    acc = rng.uniform(-0.2, 1.3, size=(72, 96, 4)).astype(np.float32)
+    acc[rng.random((72, 96)) < 0.01, 0] = np.nan
+    acc[rng.random((72, 96)) < 0.005, 2] = np.inf
+    acc[..., 1] = np.where(rng.random((72, 96)) < 0.3, rng.uniform(0, 0.004, (72, 96)), acc[..., 1]).astype(np.float32)
+    out = {"accum": acc}
+    for k, (centre, zoom, vmin, vmax, size) in enumerate(DISPLAY_CASES):
+        bg = display_background(*size)
+        out["case%d" % k] = np.array(list(centre) + [zoom] + list(vmin) + list(vmax) + list(size), np.float64)
+        out["out%d" % k] = ref_run.display(acc, centre, zoom, vmin, vmax, bg)
+    np.savez_compressed(os.path.join(GOLDEN, "display_ref.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="comma-separated fixture names (kat_<scene>, kat_nan, <image>)")
@@ -185,6 +224,12 @@ def main():
         make_kat(name, path, variant, rng)
         man["kat"][name] = {"scene": os.path.relpath(path, ROOT) if path else "builtin", "variant": variant}
         print("kat", name, flush=True)
+    if not args.only or "display" in args.only.split(","):
+        make_display()
+        man["display"] = {"fixture": "display_ref.npz", "shaders": "FullQuad.vs / FullQuad.fs",
+                          "harness": "oracle/glsl_ref/display_harness.c (compat 4.3, sRGB8_ALPHA8 target)",
+                          "cases": len(DISPLAY_CASES)}
+        print("display", flush=True)
     if not args.only or "kat_nan" in args.only.split(","):
         make_kat_nan(np.random.default_rng(7))
         man["kat"]["nan"] = {"scenes": [k for k, v in KATS.items() if v[1] == 1], "probe": "map/march with NaN dir"}

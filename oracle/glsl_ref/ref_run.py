@@ -170,3 +170,31 @@ void main()
     lines = ["image 8 8", "ui probeCount %d" % n, "run 0 0 0 0 0 0 4 %d" % gy]
     _, so = run_job(src, lines, None, ssbo_in=np.asarray(wls, np.float32), ssbo_out_n=3 * n)
     return so.reshape(n, 3)
+
+
+DISPLAY_HARNESS = os.path.join(REF_OUT, "display_harness")
+
+
+def display(accum, centre, zoom, vmin, vmax, screen):
+    """Graphics::Display (Graphics.cpp:356-390) with the reference's FullQuad.vs / FullQuad.fs on
+    llvmpipe: accum (H, W, 4) float32 (row 0 = the texture's first row), screen (h, w, 4) uint8 with
+    row 0 = top (the window's coordinates). Returns the drawn screen, row 0 = top."""
+    if not os.path.exists(DISPLAY_HARNESS):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    acc = np.ascontiguousarray(accum, np.float32)
+    H, W = acc.shape[:2]
+    scr = np.ascontiguousarray(screen, np.uint8)
+    sh, sw = scr.shape[:2]
+    with tempfile.TemporaryDirectory() as td:
+        pa, pb, po = (os.path.join(td, n) for n in ("acc.f32", "bg.rgba8", "out.rgba8"))
+        acc.tofile(pa)
+        scr[::-1].tofile(pb)   # GL rows bottom-up
+        args = [DISPLAY_HARNESS, os.path.join(shader_build.REF, "FullQuad.vs"), os.path.join(shader_build.REF, "FullQuad.fs"),
+                pa, str(W), str(H), pb, str(sw), str(sh)]
+        args += ["%.9g" % float(v) for v in (centre[0], centre[1], zoom, vmin[0], vmin[1], vmax[0], vmax[1])]
+        args.append(po)
+        r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError("display harness failed (%d): %s" % (r.returncode, r.stderr[-4000:]))
+        out = np.fromfile(po, np.uint8).reshape(sh, sw, 4)[::-1].copy()
+    return out

@@ -4,9 +4,11 @@
 // ONE_MINUS_SRC_ALPHA blend (Graphics.cpp:268-269) of the fragment's alpha 1 / 0.
 //
 // One thread per screen pixel (row 0 = top: FullQuad.vs flips y). Per pixel, in float:
-//   quad   [c - h, c + h) with h = (imageSize / 2) * zoom; fragment centre pos = pixel + 0.5
-//   uv     (pos - (c - h)) / ((c + h) - (c - h));  texel = clamp(floor(uv * imageSize))  (GL_NEAREST,
-//          Graphics.h:90-91; row 0 of the texture = accumulator row 0)
+//   quad   x in [c - h, c + h), rows y in (c - h, c + h] (GL's edge rule with FullQuad.vs's y flip),
+//          h = (imageSize / 2) * zoom; fragment centre pos = pixel + 0.5
+//   uv     (pos - (c - h)) / ((c + h) - (c - h));  texel = floor(uv * imageSize) mod imageSize
+//          (GL_NEAREST, Graphics.h:90-91, and GL_REPEAT, the default wrap; row 0 of the texture =
+//          accumulator row 0)
 //   colour texel.rgb, alpha 1 where min <= pos <= max (FullQuad.fs bounds test), else alpha 0
 //   blend  alpha 1: the sRGB-encoded colour replaces the pixel; alpha 0 and pixels outside the
 //          quad keep the caller's background
@@ -53,12 +55,16 @@ __global__ __launch_bounds__(256) void k_display(DisplayParams D) {
     const float hw = ((float)D.img_w / 2.0f) * D.zoom, hh = ((float)D.img_h / 2.0f) * D.zoom;
     const float x0 = D.cx - hw, x1 = D.cx + hw, y0 = D.cy - hh, y1 = D.cy + hh;
     const float px = (float)x + 0.5f, py = (float)y + 0.5f;
-    if (!(px >= x0 && px < x1 && py >= y0 && py < y1)) return;                  // not rasterized
+    // rasterized: GL's tie rule for a lower-left window origin (left and bottom edges in, in window
+    // coordinates; FullQuad.vs flips y, so in screen rows the quad is (y0, y1])
+    if (!(px >= x0 && px < x1 && py > y0 && py <= y1)) return;
     if (!(px >= D.min_x && px <= D.max_x && py >= D.min_y && py <= D.max_y)) return;  // alpha 0
     const float u = (px - x0) / (x1 - x0), v = (py - y0) / (y1 - y0);
-    int i = (int)floorf(u * (float)D.img_w), j = (int)floorf(v * (float)D.img_h);
-    i = i < 0 ? 0 : (i >= D.img_w ? D.img_w - 1 : i);
-    j = j < 0 ? 0 : (j >= D.img_h ? D.img_h - 1 : j);
+    // GL_REPEAT (the texture's default wrap: Framebuffer::Create sets only the filters), so the
+    // quad's included bottom row (v = 1) samples texel row 0, as the reference draws it
+    int i = (int)floorf(u * (float)D.img_w) % D.img_w, j = (int)floorf(v * (float)D.img_h) % D.img_h;
+    i += i < 0 ? D.img_w : 0;
+    j += j < 0 ? D.img_h : 0;
     const float4 t = D.accum[(size_t)j * D.img_w + i];
     const uint32_t r = srgb_byte(D.thr, t.x), g = srgb_byte(D.thr, t.y), b = srgb_byte(D.thr, t.z);
     D.rgba8[(size_t)y * D.scr_w + x] = r | (g << 8) | (b << 16) | (255u << 24);

@@ -50,9 +50,11 @@ class FrameRenderer:
     `renderer`: a raymarchrenderer_amd.Renderer (the accumulator is bound with rmr_bind_accum), or
     None with `render_fn(acc, tiles, times, first_sample)` (tests: the CPU oracle under gloo).
     `streams`: one torch.cuda.Stream per renderer. Without them each renderer gets a new torch
-    stream here (rmr_set_stream): a frame's zeroing, its render and the collective that reads it
-    must be ordered on one stream the collective waits for — a renderer left on its library-owned
-    non-blocking stream would race both."""
+    stream here (rmr_set_stream) on the accumulators' device, ordered after that device's current
+    stream (so accumulators filled there are complete before the first zeroing): a frame's zeroing,
+    its render and the collective that reads it must be ordered on one stream the collective waits
+    for — a renderer left on its library-owned non-blocking stream would race both.
+    Readers of a frame's accumulator must read on `streams[i]` of that frame or synchronize."""
 
     def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
@@ -62,8 +64,11 @@ class FrameRenderer:
             raise ValueError("accumulators must be a multiple of the renderers")
         if streams is None and render_fn is None:
             import torch
-            streams = [torch.cuda.Stream() for _ in self.rs]
+            dev = self.accs[0].device
+            cur = torch.cuda.current_stream(dev)
+            streams = [torch.cuda.Stream(device=dev) for _ in self.rs]
             for r, s in zip(self.rs, streams):
+                s.wait_stream(cur)
                 r.set_stream(s.cuda_stream)
         self.streams = list(streams) if streams is not None else None
         self.work = [None] * len(self.accs)

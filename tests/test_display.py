@@ -84,18 +84,126 @@ def test_display_rejects_wrong_screen_buffers():
     """A screen that is not (h, w, 4) RGBA8 is refused before any copy (renderer.py), and the C ABI
     refuses a buffer smaller than screen_w * screen_h * 4 bytes (rmr_display / rmr_display_device)."""
     import ctypes as C
-    from raymarchrenderer_amd import RMRError, Renderer, abi
+    from raymarchrenderer_amd import RMRError, Renderer
     from raymarchrenderer_amd._lib import lib
+    RMR_E_INVALID = -1   # rmr.h
     r = Renderer(0, 16, 16)
     try:
         with pytest.raises(ValueError):
             r.display((8.0, 8.0), 1.0, (0, 0), (16, 16), screen=np.zeros((16, 16, 3), np.uint8))
         buf = np.zeros((16, 16, 4), np.uint8)
         rc = lib().rmr_display(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, buf.ctypes.data, buf.nbytes - 1)
-        assert rc == abi.RMR_E_INVALID
+        assert rc == RMR_E_INVALID
         rc = lib().rmr_display_device(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, C.c_void_p(1), 16 * 16 * 4 - 4)
-        assert rc == abi.RMR_E_INVALID
+        assert rc == RMR_E_INVALID
         with pytest.raises(RMRError):
             r.display_device((8.0, 8.0), 1.0, (0, 0), (16, 16), 1, 16, 16, nbytes=100)
+    finally:
+        r.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# Pin to the reference itself: FullQuad.vs / FullQuad.fs run by Graphics::Display's GL state on
+# Mesa llvmpipe (oracle/glsl_ref/display_harness.c; tests/golden/display_ref.npz, generated by
+# oracle/glsl_ref/make_goldens.py --only display).
+#
+# What GL leaves to the implementation, and so the tolerance:
+# * the float -> sRGB8 encode: llvmpipe's is approximate (0.5 -> 187 where round(255 srgb(0.5)) =
+#   round(187.52) = 188): +-1 per channel;
+# * which texel GL_NEAREST picks when a fragment's exact texture coordinate lies on a texel
+#   boundary (zoom 0.5 or 1 with half-pixel offsets put every fragment there): the interpolated
+#   coordinate's rounding decides, so there either neighbour is accepted.
+# Everything else is exact: which pixels the quad covers (GL's edge rule), the FullQuad.fs bounds
+# test, the blend (pixels outside keep the background byte for byte), NaN / inf / negative / > 1
+# texels.
+# ---------------------------------------------------------------------------------------------
+def _ref_cases():
+    import os
+    from .conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "display_ref.npz"))
+    acc = g["accum"]
+    cases = []
+    k = 0
+    while "case%d" % k in g.files:
+        c = g["case%d" % k]
+        centre, zoom, vmin, vmax = (c[0], c[1]), c[2], (c[3], c[4]), (c[5], c[6])
+        size = (int(c[7]), int(c[8]))
+        cases.append((centre, zoom, vmin, vmax, size, g["out%d" % k]))
+        k += 1
+    return acc, cases
+
+
+def _background(w, h):
+    y, x = np.mgrid[0:h, 0:w]
+    bg = np.stack([(7 * x + 13 * y) % 256, (11 * x + 3 * y + 50) % 256, (5 * x + 17 * y + 99) % 256,
+                   np.full_like(x, 7)], -1)
+    return bg.astype(np.uint8)
+
+
+def _check_against_reference(got, ref, acc, centre, zoom, vmin, vmax, size):
+    H, W = acc.shape[:2]
+    bg = _background(*size)
+    drawn_ref = ref[..., 3] == 255
+    drawn_got = got[..., 3] == 255
+    # FullQuad.fs tests the interpolated varying Pos against the bounds: a pixel centre exactly on a
+    # bounds edge is decided by the interpolation's rounding (llvmpipe: either way, by case)
+    px = np.arange(size[0]) + 0.5
+    py = np.arange(size[1]) + 0.5
+    tie = (np.isin(py, [vmin[1], vmax[1]])[:, None]) | (np.isin(px, [vmin[0], vmax[0]])[None, :])
+    cov = drawn_ref != drawn_got
+    assert not (cov & ~tie).any(), "coverage differs at %d pixels" % (cov & ~tie).sum()
+    assert np.array_equal(got[~drawn_got], bg[~drawn_got]) and np.array_equal(ref[~drawn_ref], bg[~drawn_ref])
+    drawn_ref = drawn_ref & drawn_got
+    # exact texture coordinate of every pixel centre (float64), and whether it sits on a texel boundary
+    hw, hh = np.float32(W / 2) * np.float32(zoom), np.float32(H / 2) * np.float32(zoom)
+    x0, x1 = float(np.float32(centre[0]) - hw), float(np.float32(centre[0]) + hw)
+    y0, y1 = float(np.float32(centre[1]) - hh), float(np.float32(centre[1]) + hh)
+    uw = (np.arange(size[0]) + 0.5 - x0) / (x1 - x0) * W
+    vh = (np.arange(size[1]) + 0.5 - y0) / (y1 - y0) * H
+    on_u = np.abs(uw - np.round(uw)) < 1e-3
+    on_v = np.abs(vh - np.round(vh)) < 1e-3
+    thr = dref.srgb_thresholds()
+    d = np.abs(got[..., :3].astype(int) - ref[..., :3].astype(int)).max(-1)
+    ok = ~drawn_ref | (d <= 1)
+    n_boundary = 0
+    for y, x in np.argwhere(~ok):
+        assert on_u[x] or on_v[y], "pixel (%d, %d): %s vs reference %s" % (x, y, got[y, x], ref[y, x])
+        n_boundary += 1
+        iu = [int(np.round(uw[x])) - 1, int(np.round(uw[x]))] if on_u[x] else [int(np.floor(uw[x]))]
+        jv = [int(np.round(vh[y])) - 1, int(np.round(vh[y]))] if on_v[y] else [int(np.floor(vh[y]))]
+        cands = [dref.srgb8(acc[j % H, i % W, :3], thr).astype(int)
+                 for i in iu for j in jv]
+        assert any(np.abs(c - ref[y, x, :3].astype(int)).max() <= 1 for c in cands), (x, y)
+        assert any(np.abs(c - got[y, x, :3].astype(int)).max() <= 1 for c in cands), (x, y)
+    return n_boundary
+
+
+def test_display_restatement_vs_reference_llvmpipe():
+    """oracle/display.py (the restatement rmr_display is tested against byte for byte) against the
+    reference's own display pass on llvmpipe, every case."""
+    acc, cases = _ref_cases()
+    assert len(cases) >= 9
+    exact = total = 0
+    for centre, zoom, vmin, vmax, size, ref in cases:
+        got = dref.display(acc, centre, zoom, vmin, vmax, _background(*size))
+        _check_against_reference(got, ref, acc, centre, zoom, vmin, vmax, size)
+        exact += int((got == ref).all(-1).sum())
+        total += got.shape[0] * got.shape[1]
+    assert exact > 0.6 * total
+
+
+@pytest.mark.gpu
+def test_display_kernel_vs_reference_llvmpipe():
+    """rmr_display (k_display) against the reference's display pass on llvmpipe, every case."""
+    from raymarchrenderer_amd import Renderer
+    acc, cases = _ref_cases()
+    r = Renderer(0, acc.shape[1], acc.shape[0])
+    try:
+        r.write_accum(acc)
+        for centre, zoom, vmin, vmax, size, ref in cases:
+            got = r.display(centre, zoom, vmin, vmax, screen=_background(*size))
+            _check_against_reference(got, ref, acc, centre, zoom, vmin, vmax, size)
+            want = dref.display(acc, centre, zoom, vmin, vmax, _background(*size))
+            assert np.array_equal(got, want)
     finally:
         r.close()
