@@ -214,18 +214,6 @@ int rmr_set_jit(rmr_ctx* ctx, int mode);
 #define RMR_CULL_NPC 2
 #define RMR_CULL_APPROX 4
 int rmr_set_culling(rmr_ctx* ctx, int flags);
-/* Wave scheduling of the specialised kernels (results bit-identical either way):
- *   RMR_SCHED_MEGA:  (default) every wave marches and shades its own paths (deferred shading
- *                    batches)
- *   RMR_SCHED_SPLIT: per workgroup, one shading wave and seven marching waves exchange paths
- *                    through LDS rings, so shading runs full-width; applies to the kernels whose
- *                    hit point lives in the ray origin (RM1 with the fast materials, RM3) without
- *                    the nearest-primitive cache, the others keep RMR_SCHED_MEGA. Measured 17-20%
- *                    slower than RMR_SCHED_MEGA on Cornell-5, so opt-in.
- * Env RMR_SPLIT=1 selects RMR_SCHED_SPLIT at rmr_create. */
-#define RMR_SCHED_MEGA 0
-#define RMR_SCHED_SPLIT 1
-int rmr_set_schedule(rmr_ctx* ctx, int schedule);
 /* Compile the specialised kernel of a scene without a GPU (json NULL = the variant's built-in
  * scene). On success `log` receives the code-object key, otherwise the compiler log. */
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);

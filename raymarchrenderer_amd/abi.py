@@ -111,6 +111,3 @@ CULL_ESCAPE = 1
 CULL_NPC = 2
 CULL_APPROX = 4
 CULL_ALL = CULL_ESCAPE | CULL_NPC | CULL_APPROX
-# rmr_set_schedule (rmr.h)
-SCHED_MEGA = 0
-SCHED_SPLIT = 1

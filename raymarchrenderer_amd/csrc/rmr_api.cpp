@@ -109,7 +109,6 @@ struct rmr_ctx {
     // (R = 8; csg256 with the candidate grid: 15.7 -> 14.8 ms per 4 spp against R = 2)
     int full_threshold = 40 | (8 << 8);
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
-    int sched = RMR_SCHED_MEGA;    // rmr_set_schedule
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
@@ -309,7 +308,6 @@ int upload_scene(rmr_ctx* c) {
     for (const auto& p : s.prims) simple = simple && (p.type == RMR_PRIM_SPHERE || p.type == RMR_PRIM_BOX);
     const size_t n = s.prims.size();
     c->map_np = !simple || n == 0 ? -1 : (n <= 4 ? 4 : (n <= 8 ? 8 : (n <= kMaxLoopPrims ? 0 : -2)));
-    if (c->map_np >= 0 && rmr::small_npc_applies(s, c->has_prog, c->cull)) c->map_np = -2;   // (see rmr_jit.hpp)
     if (c->map_np == -2) {
         if ((r = upload_bvh(c))) return r;
     } else {
@@ -357,12 +355,11 @@ int ensure_jit(rmr_ctx* c) {
             if (std::memcmp(&prims[j], &c->jit_base[j], sizeof(rmr_prim)) != 0) c->jit_live[j] = 1;
     }
     c->jit_struct_src = struct_src;
-    const bool split = c->sched == RMR_SCHED_SPLIT && rmr::jit_split_applies(c->scene, c->has_prog, c->cull);
     // one cached primitive when the cache's full map() runs through the candidate grid (csg256: 21.5 ->
     // 17.4 ms per 4 spp against two); two with the BVH full map
     int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
     if (const char* e = std::getenv("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
-    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, split, npc_k);
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k);
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {
@@ -389,19 +386,15 @@ int ensure_jit(rmr_ctx* c) {
         c->jit_failed = true;
         return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
     }
-    k.block = split ? rmr::kSplitBlock : 256;
+    k.block = 256;
     int b = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = split ? 2 : 4;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
     // general maps without material programs, whose map() dwarfs the shading (the Mandelbulb): 8
     // (C3 +2-3%); otherwise 16 (RM1 inline sphere/box maps: 20 until the map() loop lost ~12% of its
     // instructions in round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default
     // +1.2%, tools/env_ab.py shade_t)
-    // split kernels: lanes a marching wave collects before handing finished marches over (and idle
-    // lanes before it refills)
-    if (split)
-        k.shade_t = 6;
-    else if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
+    if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
         k.shade_t = 8;
     else
         k.shade_t = 16;
@@ -852,7 +845,6 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
     if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
     if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
-    if (const char* e = std::getenv("RMR_SPLIT")) c->sched = std::atoi(e) ? RMR_SCHED_SPLIT : RMR_SCHED_MEGA;
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
@@ -1128,7 +1120,6 @@ int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
     if (r) return r;
     unsigned long long cnt[16];
     HIPCHK(c, hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
-    if (cnt[14]) return fail(c, RMR_E_HIP, "split trace kernel: a workgroup's wait timed out (" + std::to_string(cnt[14]) + ")");
     c->stats.map_evals = cnt[0];
     c->stats.map_iters = cnt[1];
     c->stats.shade_batches = cnt[2];
@@ -1302,13 +1293,6 @@ int rmr_set_culling(rmr_ctx* c, int flags) {
     if (!c || (flags & ~(RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX))) return RMR_E_INVALID;
     if (flags != c->cull) c->jit_ready = false;   // the specialised kernel depends on it
     c->cull = flags;
-    return RMR_OK;
-}
-
-int rmr_set_schedule(rmr_ctx* c, int schedule) {
-    if (!c || (schedule != RMR_SCHED_MEGA && schedule != RMR_SCHED_SPLIT)) return RMR_E_INVALID;
-    if (schedule != c->sched) c->jit_ready = false;   // the specialised kernel depends on it
-    c->sched = schedule;
     return RMR_OK;
 }
 

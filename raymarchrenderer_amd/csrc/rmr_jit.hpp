@@ -23,18 +23,8 @@ struct JitKernel {
     hipFunction_t fn = nullptr;
     int blocks_per_cu = 0;
     int shade_t = 16;           // default shading batch size for this kernel (rmr_api.cpp)
-    int block = 256;            // workgroup size (march / shade split kernels: 64 x RMR_SPLIT_WAVES)
+    int block = 256;            // workgroup size
 };
-// Workgroup size of the split kernels (rmr_trace.h trace_split: RMR_SPLIT_WAVES waves)
-constexpr int kSplitBlock = 512;
-// Small sphere/box scenes (<= 32 primitives) through the nearest-primitive cache (a one-leaf BVH in
-// the table, TableMap<-3> in the kernel) instead of the straight-line approximate map: env
-// RMR_SMALL_NPC (1: two cached primitives, 2: one), HO kernels with RMR_CULL_NPC only.
-int small_npc_mode();
-bool small_npc_applies(const CompiledScene& s, bool prog, int cull);
-
-// The split schedule applies to this specialisation (HO kernel without the nearest-primitive cache)
-bool jit_split_applies(const CompiledScene& s, bool prog, int cull);
 
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the
 // primitives' numbers are literals (fastest: +6-12% over loading them); otherwise only the scene's
@@ -43,10 +33,9 @@ bool jit_split_applies(const CompiledScene& s, bool prog, int cull);
 // cull: RMR_CULL_* bits of the context (rmr.h): approximate-then-exact map, nearest-primitive cache.
 // live (with bake): primitives j with live[j] != 0 are loaded even so (an animation's moving
 // primitives; the rest stay literals).
-// split: the march / shade split schedule where it applies (jit_split_applies).
 // npc_k: primitives per lane in the nearest-primitive cache (RMR_NPC_K: 1 or 2) of BVH scenes.
 std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
-                       const std::vector<char>* live = nullptr, bool split = true, int npc_k = 2);
+                       const std::vector<char>* live = nullptr, int npc_k = 2);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);

@@ -300,38 +300,6 @@ RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nu
     }
     return mb_de(r, dr);
 }
-// The same estimator one loop iteration at a time (the stepped map of the scene-specialised kernels,
-// trace_main): a lane's map() spreads over as many wave iterations as its own point needs, instead
-// of every lane of the wave waiting for the slowest one (C3: the bailout count varies per lane).
-// mb_step runs loop iteration s.i; true when the loop is over, with r = the final |z|.
-struct MBStep {
-    V3 z, p0;
-    float dr;
-    int i;         // loop index; -1: no map() in progress
-    V2 pre;        // opU fold of the primitives before the Mandelbulb
-};
-// RMR_MB_STEP_K loop iterations per wave pass (the per-pass begin / finish cost against the lanes'
-// different bailout counts)
-#ifndef RMR_MB_STEP_K
-#define RMR_MB_STEP_K 2   // (C3 16 spp with mb_iter8_poly: K 1 / 2 / 3 -> 17.0 / 14.6 / 14.6 ms; whole map 14.2)
-#endif
-RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, float& r, unsigned long long* cnt) {
-    (void)cnt;
-    if (iters <= 0) {   // the loop does not run: r stays 0
-        r = 0.0f;
-        return true;
-    }
-    for (int k = 0; k < RMR_MB_STEP_K; k++) {
-        r = length(s.z);
-        if (r > bail) return true;
-        RMR_COUNT_MB(cnt, active_lanes(), power);
-        mb_iter(s.z, s.dr, s.p0, power, r);
-        s.i++;
-        if (s.i >= iters) return true;
-    }
-    return false;
-}
-
 // Register file of a generated function (vec3 vars[total_vars]); indices are wave-uniform.
 struct VarFile {
     float x[RMR_MAX_VARS], y[RMR_MAX_VARS], z[RMR_MAX_VARS];
@@ -499,22 +467,16 @@ RMR_D void am_sphere(AMin& m, V3 p, V3 c, float r, float id) {
 struct BMin {
     float k1, k2, id;
 };
-#ifndef RMR_BKEY_ADD
-#define RMR_BKEY_ADD 1
-#endif
 RMR_D float bm_key(V3 p, V3 c, V3 r) {
     const V3 q = vabs(p - c) - r;
     const float k = fminf(fmaxf(q.x, fmaxf(q.y, q.z)), 0.0f);
     const V3 o = vmax0(q);
     const float l2 = dot(o, o);
-#if RMR_BKEY_ADD
     // one of the two is zero (outside: max q > 0, so k = 0; inside: every q <= 0, so len2 = 0; a
-    // positive q whose square underflows gives 0 + 0), so l2 + k is exactly the selected key, NaN for
-    // a NaN point; only -0 becomes +0, which orders, folds and square-roots the same
+    // positive q whose square underflows gives 0 + 0), so l2 + k is exactly the selected key
+    // (len2 outside, k inside), NaN for a NaN point; only -0 becomes +0, which orders, folds and
+    // square-roots the same
     return l2 + k;
-#else
-    return (l2 > 0.0f || l2 != l2) ? l2 : k;
-#endif
 }
 RMR_D void bm_box0(BMin& b, V3 p, V3 c, V3 r, float id) {
     b.k1 = bm_key(p, c, r);
@@ -689,13 +651,10 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 // point fmaxf / fminf drop the NaN: a sphere then gives -r where sd_sphere gives NaN.) Per-lane
 // index: vector loads.
 // Where the cached primitives are read from: the leaf-ordered DPrim table itself (global, per-lane
-// vector loads through the L1) or, with RMR_NPC_LDS, a copy of it staged in the workgroup's LDS at
-// kernel start (scenes of <= RMR_NPC_LDS_MAX primitives).
+// vector loads through the L1) or a copy of it staged in the workgroup's LDS at kernel start (scenes
+// of <= RMR_NPC_LDS_MAX primitives).
 // (csg256 8 spp at 6 waves / SIMD: 24.0 -> 22.2 ms with the table in LDS; at 8 waves the block's LDS
 // had to stay at 20 KiB for 8 blocks per CU)
-#ifndef RMR_NPC_LDS
-#define RMR_NPC_LDS 1
-#endif
 #ifndef RMR_NPC_LDS_MAX
 #define RMR_NPC_LDS_MAX 256
 #endif
@@ -725,24 +684,7 @@ RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
 // Seeded with the lane's cached primitive (leaf index ks, scene index js, exact distance ds, id ms;
 // ks < 0: none): visiting it first is the fold's closed form in another order, and its exact
 // distance tightens the culling bound from the first node on.
-// Inlining of the cache's rarely taken full-map paths (register pressure of the cached kernel): 0 all
-// inline; 1 the exact traversal (near ties, NaN points) is a call; 2 also the BVH traversal of lanes
-// outside the candidate grid. Measured: calls are 3.1-3.4x slower on csg256 (the call convention
-// saves the caller's live registers to scratch around every call), so 0.
-#ifndef RMR_NPC_NOINLINE
-#define RMR_NPC_NOINLINE 0
-#endif
-#if RMR_NPC_NOINLINE >= 1
-#define RMR_NPC_EXACT_ATTR __device__ __noinline__
-#else
-#define RMR_NPC_EXACT_ATTR RMR_D
-#endif
-#if RMR_NPC_NOINLINE >= 2
-#define RMR_NPC_BVH_ATTR __device__ __noinline__
-#else
-#define RMR_NPC_BVH_ATTR RMR_D
-#endif
-RMR_NPC_EXACT_ATTR V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
+RMR_D V2 map_bvh_npc_exact(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
                            bool count = true) {
     (void)count;
     typedef const __attribute__((address_space(4))) BvhNode CNode;
@@ -831,14 +773,7 @@ RMR_D float am_prim(int type, V3 p, V3 c, V3 r) {
     const V3 v = p - c;
     return __builtin_amdgcn_sqrtf(dot(v, v)) - r.x;
 }
-#ifndef RMR_NPC_APPROX
-#define RMR_NPC_APPROX 1
-#endif
-#ifndef RMR_NPC_HOIST
-#define RMR_NPC_HOIST 1
-#endif
-RMR_NPC_BVH_ATTR V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
-    if (!RMR_NPC_APPROX) return map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms);
+RMR_D V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
     typedef const __attribute__((address_space(4))) BvhNode CNode;
     CNode* nodes = (CNode*)P.bvh;
     CDPrim* pr = (CDPrim*)P.dprims;
@@ -871,15 +806,14 @@ RMR_NPC_BVH_ATTR V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float
         const int count = nodes[i].count, skip = nodes[i].skip;
         const V3 q = vmax0(vmax(lo - p, p - hi));
         const float lb2 = dot(q, q);
-        const bool need = !(lb2 > (RMR_NPC_HOIST ? t2 : radius2(u1)));
+        const bool need = !(lb2 > t2);
 #ifdef RMR_NPC_VISITS
         v_tests++;
         if (need) { if (nodes[i].count == 0) own_int++; else own_prims += (uint32_t)nodes[i].count; }
         if (__ballot(need) && nodes[i].count != 0) v_prims += (uint32_t)nodes[i].count;
 #endif
         if (!__ballot(need)) {
-            if (RMR_NPC_HOIST) lbs2 = fminf(lbs2, lb2);
-            else lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
+            lbs2 = fminf(lbs2, lb2);
             i = skip;
             continue;
         }
@@ -899,10 +833,10 @@ RMR_NPC_BVH_ATTR V2 map_bvh_npc(const KParams& P, V3 p, int& kw, int& kw2, float
             k1 = lt1 ? k : k1;
             u1 = fminf(u1, a);
         }
-        if (RMR_NPC_HOIST) t2 = radius2(u1);
+        t2 = radius2(u1);
         i = skip;
     }
-    if (RMR_NPC_HOIST) lbs = fmaf(__builtin_amdgcn_sqrtf(lbs2), 1.0f - 0x1p-20f, -P.bvh_margin);
+    lbs = fmaf(__builtin_amdgcn_sqrtf(lbs2), 1.0f - 0x1p-20f, -P.bvh_margin);
     #ifdef RMR_NPC_VISITS
     {
         uint32_t mt = 1u + 2u * own_int, mp = own_prims;
@@ -1084,105 +1018,12 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
     return d;
 }
 
-// map_bvh_npc with a per-lane traversal: every lane walks the pre-order node list with its own
-// culling decisions (the same predicate as the wave-uniform walk, !(lb2 > t^2) with t from the
-// lane's own running minimum), one node test or one primitive per loop pass, so a pass costs one
-// node test plus one primitive whatever the lanes' mix, and the loop runs as long as the busiest
-// lane's own walk instead of the union of every lane's nodes (csg256: ~26 node tests and ~16
-// primitives for the busiest lane against 76 and 81 for the wave-uniform walk, tools/npc_visits.py).
-// Nodes and primitives are per-lane vector loads. The closed form of the fold is order- and
-// subset-free (every skipped primitive is strictly above the minimum), so the map() values are the
-// wave walk's; only the cache outputs (kw, kw2, sb: a lane's own evaluated set) may differ, and
-// those only choose between two exact paths.
-#ifndef RMR_NPC_LANE
-#define RMR_NPC_LANE 0   // csg256 4 spp: 43.2 ms against 36.2 for the wave walk (dependent per-lane loads)
-#endif
-RMR_D V2 map_bvh_npc_lane(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms) {
-    const float R2 = P.am_r2;
-    float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff(), lbs = __builtin_inff();
-    int k1 = -1, k2 = -1;
-    if (ks >= 0) {
-        u1 = ds;
-        k1 = ks;
-    }
-    const int n_nodes = P.n_nodes;
-    int i = 0, k = 0, kend = 0;   // next node; pending primitives [k, kend) of the current leaf
-    for (;;) {
-        const bool prim = k < kend;
-        if (!__ballot(prim || i < n_nodes)) break;
-        if (prim) {
-            const float4* q = (const float4*)(P.dprims + k);
-            const float4 a = q[0], b = q[1];   // c.xyz r.x | r.yz type|index<<8 mat_id
-            if (k != ks) {
-                const int type = __float_as_int(b.z) & 0xff;
-                const float av = am_prim(type, p, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y));
-#ifdef RMR_COUNT_FLOPS
-                const uint64_t nb = (uint64_t)__popcll(__ballot(type == RMR_PRIM_BOX));
-                RMR_COUNT(P.counters, nb, 22 + 2, 1);
-                RMR_COUNT(P.counters, active_lanes() - nb, 10 + 2, 1);
-#endif
-                const bool lt1 = av < u1, lt2 = av < u2;
-                u3 = __builtin_amdgcn_fmed3f(u2, av, u3);
-                u2 = __builtin_amdgcn_fmed3f(u1, av, u2);
-                k2 = lt1 ? k1 : (lt2 ? k : k2);
-                k1 = lt1 ? k : k1;
-                u1 = fminf(u1, av);
-            }
-            k++;
-        } else if (i < n_nodes) {
-            const float4* nq = (const float4*)(P.bvh + i);
-            const float4 n0 = nq[0], n1 = nq[1];   // lo.xyz first | hi.xyz count
-            const int skip = __float_as_int(nq[2].x);
-            const V3 q = vmax0(vmax(v3(n0.x, n0.y, n0.z) - p, p - v3(n1.x, n1.y, n1.z)));
-            const float lb2 = dot(q, q);
-            const float ub = fminf(P.max_dist, u1 + fmaf(fabsf(u1) + R2, 0x1p-20f, 0x1p-39f));
-            const float t = fmaxf(ub + fmaf(fabsf(ub), 0x1p-18f, P.bvh_margin), P.bvh_margin);
-            const int count = __float_as_int(n1.w);
-            if (lb2 > t * t) {
-                lbs = fminf(lbs, fmaf(__builtin_amdgcn_sqrtf(lb2), 1.0f - 0x1p-20f, -P.bvh_margin));
-                i = skip;
-            } else if (count == 0) {
-                i++;
-            } else {
-                k = __float_as_int(n0.w);
-                kend = k + count;
-                i = skip;
-            }
-        }
-    }
-    const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
-    const bool alone = (u2 == __builtin_inff()) && (u1 < __builtin_inff());
-    const bool uniq = (alone || u2 - u1 > margin) && k1 >= 0;
-    V2 d = v2(P.max_dist, -1.0f);
-    if (uniq) {
-        float mid;
-        int j;
-        const float dw = (k1 == ks) ? ds : prim_dist(P, k1, p, mid, j);
-        if (k1 == ks) mid = ms;
-        opu(d, dw, mid);
-        kw = (dw > P.max_dist) ? -1 : k1;
-        const float v = (RMR_NPC_K >= 2 && k2 >= 0) ? u3 : u2;
-        const float vlb = v - fmaf(fabsf(v) + R2, 0x1p-20f, 0x1p-39f);
-        kw2 = (RMR_NPC_K >= 2 && k2 >= 0) ? k2 : k1;
-        sb = fminf(vlb, lbs);
-    }
-    if (__ballot(!uniq)) {
-        if (!uniq) d = map_bvh_npc_exact(P, p, kw, kw2, sb, ks, js, ds, ms, false);
-    }
-    return d;
-}
-
 template <int NP>
 struct TableMap {
     // NP == -3: the BVH map with the nearest-primitive cache (trace_main's kCache path)
     static constexpr bool kCache = (NP == -3);
     // the map counts its own executed work (BVH traversals skip primitives; see RMR_COUNT_FLOPS)
     static constexpr bool kCounts = (NP == -2 || NP == -3);
-    // map() one Mandelbulb loop iteration at a time (begin / step / finish: the specialised kernels)
-    static constexpr bool kStepped = false;
-    static RMR_D void begin(const KParams&, V3, MBStep&) {}
-    static RMR_D bool step(const KParams&, MBStep&, float&) { return true; }
-    static RMR_D V2 finish(const KParams& P, V3, const MBStep&, float) { return v2(P.max_dist, -1.0f); }
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
@@ -1191,8 +1032,7 @@ struct TableMap {
     }
     static RMR_D V2 full(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
                          const float4* dtab) {
-        if (RMR_NPC_LANE && RMR_NPC_APPROX) return map_bvh_npc_lane(P, p, kw, kw2, sb, ks, js, ds, ms);
-        if (RMR_NPC_APPROX && P.grid) return map_grid_npc(P, p, kw, kw2, sb, ks, js, ds, ms, dtab);
+        if (P.grid) return map_grid_npc(P, p, kw, kw2, sb, ks, js, ds, ms, dtab);
         return map_bvh_npc(P, p, kw, kw2, sb, ks, js, ds, ms);
     }
 };
@@ -1481,12 +1321,9 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
 // distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
-#ifndef RMR_BRANCHLESS_UPDATE
-#define RMR_BRANCHLESS_UPDATE 1
-#endif
 template <bool HO, bool CACHE = false>
 RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
-    if constexpr (HO && !CACHE && RMR_BRANCHLESS_UPDATE) {   // (cache kernels: A/B neutral-negative)
+    if constexpr (HO && !CACHE) {   // (cache kernels: A/B neutral-negative)
         // HO kernels (no shadow rays): the same state transitions as below as per-lane selects
         const float dist = L.inside ? -m.x : m.x;
         const bool hit = dist < 0.001f;
@@ -1951,9 +1788,6 @@ RMR_D void shade(const KParams& P, Lane& L) {
 // Lane state that only shading, refills and the end of a trace read (RM1 throughput / RM3 power and
 // hero wavelength, RNG chain, unit, channel, bounce count): parked in LDS, one word per lane per
 // field (conflict-free), while the nearest-primitive cache's inner march loop runs.
-#ifndef RMR_NPC_STASH
-#define RMR_NPC_STASH 1
-#endif
 constexpr int kColdWords = 8;
 template <int VAR>
 RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
@@ -2016,31 +1850,16 @@ constexpr int trace_waves() {
     return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
 }
 
-#ifndef RMR_UNIFIED_POINT
-#define RMR_UNIFIED_POINT 1
-#endif
-#if RMR_UNIFIED_POINT   // HO kernels (A/B: C2 +1%; the RM2 kernel was slower with it)
+// the map() point of an active lane: one select per component in HO kernels (A/B: C2 +1%; the RM2
+// kernel was slower with it)
 #define RMR_MARCH_POINT(L) (HO ? march_point<HO>(L) : ((L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o)))
-#else
-#define RMR_MARCH_POINT(L) ((L.phase == PH_NORMAL) ? probe_point<HO>(L) : vfma(L.d, L.t, L.o))
-#endif
 #ifndef RMR_CHUNK
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
 #ifndef RMR_CHUNK_CACHE
 #define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
-#ifndef RMR_INNER_MARCH
-#define RMR_INNER_MARCH 1
-#endif
-#ifndef RMR_WAVE_COUNT64
-#define RMR_WAVE_COUNT64 0
-#endif
-#if RMR_WAVE_COUNT64
-typedef uint64_t WCount;
-#else
 typedef uint32_t WCount;
-#endif
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
@@ -2049,10 +1868,7 @@ RMR_D void trace_main(const KParams& P) {
     init_probe(L);
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
-    WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, steps = 0;
-    MBStep mbs;   // stepped map() state (MAP::kStepped)
-    mbs.i = -1;
-    bool maps_done = false;
+    WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
     constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
@@ -2072,9 +1888,8 @@ RMR_D void trace_main(const KParams& P) {
 #endif
     __shared__ ChunkRay s_ray[4][CHUNK];   // per wave (256-thread blocks = 4 waves)
     // cache kernels: the lane's shading-only state during the inner march loop (cold_put / cold_get)
-    constexpr bool kStash = MAP::kCache && HO && RMR_NPC_STASH;
+    constexpr bool kStash = MAP::kCache && HO;
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
-#if RMR_NPC_LDS
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
     const bool dp_lds = MAP::kCache && P.n_prims <= RMR_NPC_LDS_MAX;
@@ -2084,10 +1899,6 @@ RMR_D void trace_main(const KParams& P) {
     }
 #define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_at(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
 #define RMR_DTAB (dp_lds ? (const float4*)s_dp : (const float4*)P.dprims)
-#else
-#define RMR_PRIM_DIST(k, p, mid, j) prim_dist(P, k, p, mid, j)
-#define RMR_DTAB ((const float4*)P.dprims)
-#endif
     const int wv = (threadIdx.x >> 6) & 3;
     uint32_t chunk_base = 0;
 #ifdef RMR_WAVE_TIMES   // counters [9] ~min start, [11] ~min / [10] max queue exhaustion, [12] ~min /
@@ -2213,9 +2024,6 @@ RMR_D void trace_main(const KParams& P) {
                     const float sum = p.x + p.y + p.z;   // NaN for a NaN (or +-inf mixed) point
                     pfin = sum == sum;
                     ok = pfin && (L.cs - delta - npc_eps(P, p) > Fm);
-#ifdef RMR_NPC_ALWAYS_FULL   // experiment: every map() through the full path (the candidate grid)
-                    ok = false;
-#endif
                 }
                 const uint64_t okm = __ballot(act1 && ok);
                 const uint64_t fm = __ballot(act1 && !ok);
@@ -2258,42 +2066,13 @@ RMR_D void trace_main(const KParams& P) {
                 maps += (WCount)__popcll(dm);
                 iters += dm ? 1 : 0;
                 const uint64_t sm = __ballot(is_shade(L.phase));
-                go = RMR_INNER_MARCH && __ballot(is_active(L.phase)) && __popcll(sm) < T;
+                go = __ballot(is_active(L.phase)) && __popcll(sm) < T;
             }
             if constexpr (kStash) {
                 if (amask) {
                     __asm__ volatile("" ::: "memory");
                     cold_get<VAR>(s_cold, (int)threadIdx.x, L);
                 }
-            }
-        } else if (MAP::kStepped && amask) {
-            // stepped map() (the Mandelbulb one loop iteration per wave iteration): every active lane
-            // runs one estimator iteration per pass; a lane whose estimator finishes completes its
-            // map() (the other primitives and the fold) and applies it, and starts its next map()
-            // in the following pass. Same operations per lane as MAP::eval.
-            uint64_t am = amask;
-            for (;;) {
-                if (is_active(L.phase)) {
-                    if (mbs.i < 0) MAP::begin(P, RMR_MARCH_POINT(L), mbs);
-                    float r;
-                    if (MAP::step(P, mbs, r)) {
-                        if constexpr (!MAP::kCounts)
-                            RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
-                        const V2 m = MAP::finish(P, RMR_MARCH_POINT(L), mbs, r);
-                        mbs.i = -1;
-                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                        else march_update<HO>(P, L, m);
-                        maps_done = true;
-                    }
-                }
-                maps += (WCount)__popcll(__ballot(maps_done));
-                maps_done = false;
-                steps += (WCount)__popcll(am);
-                iters++;
-                if (!RMR_INNER_MARCH) break;
-                const uint64_t sm = __ballot(is_shade(L.phase));
-                am = __ballot(is_active(L.phase));
-                if (!am || __popcll(sm) >= T) break;
             }
         } else if (amask) {
             // map() steps back to back until a shading batch is due or no lane is active: idle lanes
@@ -2312,7 +2091,6 @@ RMR_D void trace_main(const KParams& P) {
                 }
                 lmaps += (uint32_t)__popcll(am);
                 liters++;
-                if (!RMR_INNER_MARCH) break;
                 const uint64_t sm = __ballot(is_shade(L.phase));
                 am = __ballot(is_active(L.phase));
                 if (!am || __popcll(sm) >= T) break;
@@ -2340,16 +2118,15 @@ RMR_D void trace_main(const KParams& P) {
         const bool last = live == 0 && exhausted;
         // (an inner loop adds at most 64 x its iterations to `maps`; a flush every 2^30 keeps every
         // 32-bit counter far from wrapping between two checks)
-        if (last || ((maps | steps | shaded) >> 30) != 0) {
+        if (last || ((maps | shaded) >> 30) != 0) {
             if (__lane_id() == 0) {
                 atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
                 atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
                 atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
                 if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
-                if (MAP::kStepped) atomicAdd(P.counters + 3, (unsigned long long)steps);   // lane-level estimator steps
                 atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
             }
-            maps = iters = shades = fulls = shaded = steps = 0;
+            maps = iters = shades = fulls = shaded = 0;
         }
         if (last) break;
     }
@@ -2371,502 +2148,6 @@ RMR_D void trace_main(const KParams& P) {
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// March / shade split (persistent HO kernels without the nearest-primitive cache: RM1 with the fast
-// materials, RM3; the hipRTC kernels, rmr_jit.cpp). In trace_main every wave both marches and
-// shades: shading batches run with the ~20 lanes that wait (a quarter to a third of the wave) while
-// those lanes sit out map() iterations. Here a workgroup of RMR_SPLIT_WAVES waves has one shading
-// wave and RMR_SPLIT_WAVES - 1 marching waves that exchange paths through LDS rings:
-//  * a marching wave only runs map() iterations (march steps and getNormal probes). A lane whose
-//    march ends (HIT: normal done, or MISS) is pushed to the wave's hit ring and refilled from the
-//    wave's ray ring;
-//  * the shading wave pops hits into its free lanes from every hit ring and shades them full-width,
-//    starts fresh units (primary rays, begin_trace) in lanes left free, and pushes every new ray
-//    (bounce or primary) to the ray rings. It runs at raised priority: a marching wave waits for
-//    it, never the other way round.
-// Each path runs exactly the trace_main arithmetic (the same functions on the same Lane state), so
-// every sample is bit-identical; only which lane and which wave executes a step changes.
-// Rings are single-producer single-consumer (head/tail in LDS, workgroup-scope release/acquire).
-// No deadlock: the shading wave starts a path only while the paths in flight stay below
-// 64 x waves + 2 x rings x RMR_SPLIT_RING - 1, so the hit rings, the ray rings, the marching lanes
-// and the shading lanes can never all be full at once. Every wait is also bounded in time
-// (RMR_SPLIT_WAIT shader clocks without progress): the workgroup then exits and counts the event in
-// P.counters[14], which the host reports as an error.
-// ------------------------------------------------------------------------------------------
-#ifndef RMR_SPLIT_WAVES
-#define RMR_SPLIT_WAVES 8   // waves per workgroup: 1 shading + RMR_SPLIT_WAVES - 1 marching
-#endif
-#ifndef RMR_SPLIT_RING
-#define RMR_SPLIT_RING 32   // entries of each marching wave's ray ring and hit ring (power of two)
-#endif
-#ifndef RMR_SPLIT_WAIT
-#define RMR_SPLIT_WAIT (1ull << 31)
-#endif
-#ifndef RMR_SPLIT_PRIO
-#define RMR_SPLIT_PRIO 2
-#endif
-#ifndef RMR_SPLIT_SLEEP
-#define RMR_SPLIT_SLEEP 2   // s_sleep units (64 clocks) of the shading wave's idle poll
-#endif
-constexpr int kSplitMarch = RMR_SPLIT_WAVES - 1;
-constexpr uint32_t kRingMask = RMR_SPLIT_RING - 1;
-static_assert((RMR_SPLIT_RING & (RMR_SPLIT_RING - 1)) == 0, "ring size must be a power of two");
-struct RayRec { float4 a, b, c, d; };      // o.xyz texit | d.xyz flags | rc gxt gyt unit | color / power wl, bounces
-struct HitRec { float4 a, b, c, d, e; };   // o.xyz mid | d.xyz flags | rc gxt gyt unit | color.., bounces | nrm.xyz t
-struct SplitLds {
-    RayRec ray[kSplitMarch][RMR_SPLIT_RING];
-    HitRec hit[kSplitMarch][RMR_SPLIT_RING];
-    uint32_t ray_tail[kSplitMarch], ray_head[kSplitMarch], hit_tail[kSplitMarch], hit_head[kSplitMarch];
-    uint32_t done;     // 1: every path of the workgroup finished; 2: a wait timed out
-    uint32_t events;   // hand-overs and refills of the marching waves (the shading wave's idle poll)
-};
-RMR_D uint32_t lds_acquire(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-RMR_D void lds_release(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// flags word: phase (bits 0-3), chan + 1 (4-7), inside (8)
-RMR_D float pack_flags(const Lane& L) {
-    return __int_as_float((L.phase & 15) | ((L.chan + 1) << 4) | ((int)L.inside << 8));
-}
-RMR_D void unpack_flags(Lane& L, float f) {
-    const int v = __float_as_int(f);
-    L.phase = v & 15;
-    L.chan = ((v >> 4) & 15) - 1;
-    L.inside = ((v >> 8) & 1) != 0;
-}
-template <int VAR>
-RMR_D float4 pack_payload(const Lane& L) {   // throughput (RM1 color, RM3 power + hero wavelength), bounces
-    if constexpr (VAR == RMR_VARIANT_RM3) return make_float4(L.power, __uint_as_float(L.wl), 0.0f, __int_as_float(L.bounces));
-    else return make_float4(L.color.x, L.color.y, L.color.z, __int_as_float(L.bounces));
-}
-template <int VAR>
-RMR_D void unpack_payload(Lane& L, float4 v) {
-    if constexpr (VAR == RMR_VARIANT_RM3) {
-        L.power = v.x;
-        L.wl = __float_as_uint(v.y);
-    } else {
-        L.color = v3(v.x, v.y, v.z);
-    }
-    L.bounces = __float_as_int(v.w);
-}
-template <int VAR>
-RMR_D void put_ray(RayRec& r, const Lane& L) {
-    r.a = make_float4(L.o.x, L.o.y, L.o.z, L.texit);
-    r.b = make_float4(L.d.x, L.d.y, L.d.z, pack_flags(L));
-    r.c = make_float4(L.rc, L.gxt, L.gyt, __uint_as_float(L.unit));
-    r.d = pack_payload<VAR>(L);
-}
-template <int VAR>
-RMR_D void get_ray(Lane& L, const RayRec& r) {   // a ray as start_march left it: t = 0, ctr = 0
-    const float4 a = r.a, b = r.b, c = r.c, d = r.d;
-    L.o = v3(a.x, a.y, a.z);
-    L.texit = a.w;
-    L.d = v3(b.x, b.y, b.z);
-    unpack_flags(L, b.w);
-    L.rc = c.x; L.gxt = c.y; L.gyt = c.z; L.unit = __float_as_uint(c.w);
-    unpack_payload<VAR>(L, d);
-    L.t = 0.0f;
-    L.ctr = 0;
-}
-template <int VAR>
-RMR_D void put_hit(HitRec& h, const Lane& L) {
-    h.a = make_float4(L.o.x, L.o.y, L.o.z, L.mid);
-    h.b = make_float4(L.d.x, L.d.y, L.d.z, pack_flags(L));
-    h.c = make_float4(L.rc, L.gxt, L.gyt, __uint_as_float(L.unit));
-    h.d = pack_payload<VAR>(L);
-    h.e = make_float4(L.nrm.x, L.nrm.y, L.nrm.z, L.t);
-}
-template <int VAR>
-RMR_D void get_hit(Lane& L, const HitRec& h) {
-    const float4 a = h.a, b = h.b, c = h.c, d = h.d, e = h.e;
-    L.o = v3(a.x, a.y, a.z);
-    L.mid = a.w;
-    L.d = v3(b.x, b.y, b.z);
-    unpack_flags(L, b.w);
-    L.rc = c.x; L.gxt = c.y; L.gyt = c.z; L.unit = __float_as_uint(c.w);
-    unpack_payload<VAR>(L, d);
-    L.nrm = v3(e.x, e.y, e.z);
-    L.t = e.w;
-    L.ctr = 0;
-}
-RMR_D uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// A pair of ring index arrays (tails, heads) of a workgroup, read in one LDS round trip (relaxed
-// loads, then one acquire fence), as wave-uniform (scalar) values.
-RMR_D void ring_idx(const uint32_t* tails, const uint32_t* heads, uint32_t (&t)[kSplitMarch], uint32_t (&h)[kSplitMarch]) {
-#pragma unroll
-    for (int w = 0; w < kSplitMarch; w++) {
-        t[w] = __hip_atomic_load(&tails[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        h[w] = __hip_atomic_load(&heads[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-    for (int w = 0; w < kSplitMarch; w++) {
-        t[w] = __builtin_amdgcn_readfirstlane(t[w]);
-        h[w] = __builtin_amdgcn_readfirstlane(h[w]);
-    }
-}
-// Spread `want` items over the rings, ring rr first: ring w gets take[w] <= avail[w], in rotated
-// order; lane `rank` (< the total taken) is told its ring `mw` and its offset `off` in that ring's
-// share. Static indices only (no register-array indexing by a variable).
-RMR_D uint32_t ring_spread(const uint32_t (&avail)[kSplitMarch], uint32_t want, uint32_t rr, uint32_t rank,
-                           uint32_t (&take)[kSplitMarch], int& mw, uint32_t& off) {
-    uint32_t before_rr = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kSplitMarch; w++) {
-        before_rr += (uint32_t)w < rr ? avail[w] : 0u;
-        total += avail[w];
-    }
-    uint32_t pre = 0;   // sum of avail over rings w' < w
-    mw = -1;
-    off = 0;
-    uint32_t got = 0;
-#pragma unroll
-    for (int w = 0; w < kSplitMarch; w++) {
-        const uint32_t start = (uint32_t)w >= rr ? pre - before_rr : pre + (total - before_rr);
-        const uint32_t room = want > start ? want - start : 0u;
-        take[w] = avail[w] < room ? avail[w] : room;
-        if (rank >= start && rank < start + take[w]) { mw = w; off = rank - start; }
-        got += take[w];
-        pre += avail[w];
-    }
-    return got;
-}
-
-#ifdef RMR_SPLIT_STATS   // diagnostics (RMR_JIT_OPTS=-DRMR_SPLIT_STATS): cycle split of the two roles
-#define RMR_SSTAT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define RMR_SSTAT(v)
-#endif
-#ifndef RMR_SPLIT_QLOW
-#define RMR_SPLIT_QLOW (kSplitMarch * RMR_SPLIT_RING / 2)   // queued rays below which partial batches run
-#endif
-#ifndef RMR_SPLIT_INFLIGHT   // paths a workgroup keeps in flight (marching lanes + a batch + queued rays)
-#define RMR_SPLIT_INFLIGHT (64 * RMR_SPLIT_WAVES + kSplitMarch * RMR_SPLIT_RING / 2)
-#endif
-// Ray-ring shares that level the rings' occupancies (water filling): ring w may take
-// max(0, min(lv, RING) - occ[w]) with the smallest level lv that places `want` rays (or all free slots).
-RMR_D void ring_level(const uint32_t (&occ)[kSplitMarch], uint32_t want, uint32_t (&avail)[kSplitMarch]) {
-    uint32_t lo = 0, hi = RMR_SPLIT_RING;
-    while (lo < hi) {
-        const uint32_t lv = (lo + hi) >> 1;
-        uint32_t f = 0;
-#pragma unroll
-        for (int w = 0; w < kSplitMarch; w++) f += lv > occ[w] ? lv - occ[w] : 0u;
-        if (f >= want) hi = lv;
-        else lo = lv + 1;
-    }
-#pragma unroll
-    for (int w = 0; w < kSplitMarch; w++) avail[w] = lo > occ[w] ? lo - occ[w] : 0u;
-}
-
-// the shading wave of a workgroup
-template <int VAR, class MATS>
-RMR_D void split_shade(const KParams& P, SplitLds& S) {
-    constexpr bool HO = true;
-    __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
-    Lane L;
-    L.phase = PH_IDLE;
-    L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
-    init_probe(L);
-    const uint64_t n_units = P.n_units;
-    const uint32_t cap = 64u * RMR_SPLIT_WAVES + 2u * kSplitMarch * RMR_SPLIT_RING - 1u;
-    const uint32_t target = (uint32_t)RMR_SPLIT_INFLIGHT < cap ? (uint32_t)RMR_SPLIT_INFLIGHT : cap;
-    uint32_t in_flight = 0, rr = 0;
-    bool exhausted = false;
-    uint64_t shades = 0, shaded = 0;
-    uint64_t t_prog = __builtin_amdgcn_s_memtime();   // start of the current wait (no progress)
-    bool waiting = false;
-#ifdef RMR_SPLIT_STATS
-    uint64_t cyc_hit = 0, cyc_fresh = 0, n_hitb = 0, n_freshb = 0;
-    const uint64_t c_begin = t_prog;
-#endif
-    uint32_t last_ev = 0xffffffffu;   // S.events at the last iteration without progress
-    for (;;) {
-        bool progress = false, hb = false, fb = false;
-        const uint32_t ev = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&S.events, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (ev == last_ev) {   // nothing to do then, and no marching wave has acted since
-            if (lds_acquire(&S.done) == 2u) break;
-            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
-                if (__lane_id() == 0) {
-                    lds_release(&S.done, 2u);
-                    atomicAdd(P.counters + 14, 1ull);
-                }
-                break;
-            }
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_s_sleep(RMR_SPLIT_SLEEP);
-            __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
-            continue;
-        }
-        uint32_t ht[kSplitMarch], hh[kSplitMarch];
-        uint32_t H = 0, Q = 0;
-        {
-            uint32_t rt[kSplitMarch], rh[kSplitMarch];
-            ring_idx(S.ray_tail, S.ray_head, rt, rh);
-            ring_idx(S.hit_tail, S.hit_head, ht, hh);
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++) { H += ht[w] - hh[w]; Q += rt[w] - rh[w]; }
-        }
-        const uint64_t idle = __ballot(L.phase == PH_IDLE);
-        const uint32_t nidle = (uint32_t)__popcll(idle), rank = lane_rank(idle);
-        const uint32_t pend = 64u - nidle;   // lanes holding a ray not yet pushed
-        const bool starving = Q + pend < (uint32_t)RMR_SPLIT_QLOW;
-        RMR_SSTAT(c0);
-        if (nidle && H && (H >= nidle || starving || exhausted)) {
-            // 1. a shading batch: hits into the free lanes, from every hit ring (ring rr first)
-            uint32_t avail[kSplitMarch], take[kSplitMarch];
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++) avail[w] = ht[w] - hh[w];
-            int mw;
-            uint32_t off;
-            ring_spread(avail, nidle, rr, rank, take, mw, off);
-            uint32_t slot = 0;
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++) slot = mw == w ? hh[w] + off : slot;
-            if (L.phase == PH_IDLE && mw >= 0) get_hit<VAR>(L, S.hit[mw][slot & kRingMask]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++)
-                if (take[w]) __hip_atomic_store(&S.hit_head[w], hh[w] + take[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            rr = rr + 1 == (uint32_t)kSplitMarch ? 0 : rr + 1;
-            progress = hb = true;
-        } else if (nidle && !exhausted && in_flight < target) {
-            // 2. fresh units (primary rays) into the free lanes, up to the in-flight target
-            uint32_t take = nidle < target - in_flight ? nidle : target - in_flight;
-            if (take) {
-                unsigned long long b = 0;
-                if (__lane_id() == 0) b = atomicAdd(P.queue, (unsigned long long)take);
-                b = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-                    (unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)b);
-                if (L.phase == PH_IDLE && rank < take && b + rank < n_units)
-                    begin_trace<VAR, HO>(P, L, (uint32_t)(b + rank), true);
-                exhausted = b + take >= n_units;
-                in_flight += (uint32_t)__popcll(__ballot(L.phase != PH_IDLE)) - pend;
-                progress = fb = true;
-            }
-        }
-        RMR_SSTAT(c1);
-        // 3. shade until every lane is free or holds a new ray (a ray may miss at once: escape bound;
-        // a path can also be done straight from begin_trace: zero bounces)
-        for (;;) {
-            const uint64_t fin = __ballot(L.phase == PH_DONE);
-            in_flight -= (uint32_t)__popcll(fin);
-            if (L.phase == PH_DONE) L.phase = PH_IDLE;
-            const uint64_t sm = __ballot(is_shade(L.phase));
-            if (!sm) break;
-            shades++;
-            shaded += (uint64_t)__popcll(sm);
-            if (is_shade(L.phase)) shade<VAR, false, MATS>(P, L);
-            const bool restart = (L.phase == PH_RESTART);
-            if (__ballot(restart)) {
-                if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
-            }
-        }
-        RMR_SSTAT(c2);
-#ifdef RMR_SPLIT_STATS
-        (void)c1;
-        if (hb) { n_hitb++; cyc_hit += c2 - c0; }
-        if (fb) { n_freshb++; cyc_fresh += c2 - c0; }
-#else
-        (void)hb; (void)fb;
-#endif
-        // 4. new rays to the ray rings (ring rr first; consecutive rays of a batch stay together)
-        const uint64_t pm = __ballot(L.phase == PH_MARCH);
-        if (pm) {
-            uint32_t rt[kSplitMarch], rh[kSplitMarch], avail[kSplitMarch], take[kSplitMarch];
-            ring_idx(S.ray_tail, S.ray_head, rt, rh);
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++) avail[w] = rt[w] - rh[w];   // occupancy
-            ring_level(avail, (uint32_t)__popcll(pm), avail);
-            int mw;
-            uint32_t off;
-            const uint32_t got = ring_spread(avail, (uint32_t)__popcll(pm), rr, lane_rank(pm), take, mw, off);
-            uint32_t slot = 0;
-#pragma unroll
-            for (int w = 0; w < kSplitMarch; w++) slot = mw == w ? rt[w] + off : slot;
-            if (L.phase == PH_MARCH && mw >= 0) {
-                put_ray<VAR>(S.ray[mw][slot & kRingMask], L);
-                L.phase = PH_IDLE;
-            }
-            if (got) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-                for (int w = 0; w < kSplitMarch; w++)
-                    if (take[w]) __hip_atomic_store(&S.ray_tail[w], rt[w] + take[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                progress = true;
-            }
-        }
-        if (exhausted && in_flight == 0) {
-            if (__lane_id() == 0) lds_release(&S.done, 1u);
-            break;
-        }
-        if (progress) {
-            waiting = false;
-            last_ev = 0xffffffffu;
-        } else {
-            last_ev = ev;
-            if (!waiting) {
-                waiting = true;
-                t_prog = __builtin_amdgcn_s_memtime();
-            }
-            if (lds_acquire(&S.done) == 2u) break;
-            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
-                if (__lane_id() == 0) {
-                    lds_release(&S.done, 2u);
-                    atomicAdd(P.counters + 14, 1ull);
-                }
-                break;
-            }
-            __builtin_amdgcn_s_setprio(0);   // polling: at the marching waves' priority
-            __builtin_amdgcn_s_sleep(RMR_SPLIT_SLEEP);
-            __builtin_amdgcn_s_setprio(RMR_SPLIT_PRIO);
-        }
-    }
-    if (__lane_id() == 0) {
-        atomicAdd(P.counters + 2, (unsigned long long)shades);
-        atomicAdd(P.counters + 8, (unsigned long long)shaded);
-#ifdef RMR_SPLIT_STATS
-        atomicAdd(P.counters + 4, (unsigned long long)n_hitb);
-        atomicAdd(P.counters + 5, (unsigned long long)n_freshb);
-        atomicAdd(P.counters + 6, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
-        atomicAdd(P.counters + 7, (unsigned long long)cyc_hit);
-        atomicAdd(P.counters + 9, (unsigned long long)cyc_fresh);
-#endif
-    }
-}
-
-// a marching wave of a workgroup (ring index w). One loop iteration = one map() step for every
-// active lane; the ray ring's tail is read (relaxed) at the top of the iteration and used after the
-// step, so its latency hides behind the map. Finished marches are handed over once T lanes wait (or
-// no lane is active); idle lanes are refilled once TR of them wait (or no lane is active).
-template <int VAR, class MAP>
-RMR_D void split_march(const KParams& P, SplitLds& S, int w) {
-    constexpr bool HO = true;
-    Lane L;
-    L.phase = PH_IDLE;
-    L.cw = 0; L.cw2 = 0; L.cs = -__builtin_inff(); L.cta = 0.0f;
-    init_probe(L);
-    uint32_t ray_head = 0, hit_tail = 0, hit_head = 0;   // hit_head: last value seen (the shading wave owns it)
-    uint64_t maps = 0, iters = 0;
-    const int T = P.shade_threshold, TR = P.refill_threshold;
-    uint64_t t_prog = __builtin_amdgcn_s_memtime();   // start of the current wait (no progress)
-    bool waiting = false;
-#ifdef RMR_SPLIT_STATS
-    uint64_t cyc_starved = 0, last_c0 = t_prog;
-    bool last_starved = false;
-    const uint64_t c_begin = t_prog;
-#endif
-    for (;;) {
-        bool progress = false;
-#ifdef RMR_SPLIT_STATS
-        RMR_SSTAT(c0);
-        if (last_starved) cyc_starved += c0 - last_c0;
-        last_c0 = c0;
-#endif
-        const uint32_t ray_tail = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&S.ray_tail[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        uint64_t am = __ballot(is_active(L.phase));
-#ifdef RMR_SPLIT_STATS
-        last_starved = am == 0;
-#endif
-        if (am) {   // one map() step
-            if (is_active(L.phase)) {
-                const V3 p = RMR_MARCH_POINT(L);
-                if constexpr (!MAP::kCounts)
-                    RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
-                const V2 m = MAP::eval(P, p);
-                if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                else march_update<HO>(P, L, m);
-            }
-            maps += (uint64_t)__popcll(am);
-            iters++;
-            am = __ballot(is_active(L.phase));
-            progress = true;
-        }
-        // hand finished marches to the shading wave
-        const uint64_t sm = __ballot(is_shade(L.phase));
-        if (sm && (__popcll(sm) >= T || am == 0)) {
-            const uint32_t nsm = (uint32_t)__popcll(sm);
-            if (RMR_SPLIT_RING - (hit_tail - hit_head) < nsm) hit_head = __builtin_amdgcn_readfirstlane(lds_acquire(&S.hit_head[w]));
-            const uint32_t freeh = RMR_SPLIT_RING - (hit_tail - hit_head);
-            const uint32_t n = freeh < nsm ? freeh : nsm;
-            if (n) {
-                const uint32_t rank = lane_rank(sm);
-                if (is_shade(L.phase) && rank < n) {
-                    put_hit<VAR>(S.hit[w][(hit_tail + rank) & kRingMask], L);
-                    L.phase = PH_IDLE;
-                }
-                hit_tail += n;
-                lds_release(&S.hit_tail[w], hit_tail);
-                if (__lane_id() == 0) __hip_atomic_fetch_add(&S.events, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                progress = true;
-            }
-        }
-        // refill idle lanes from the ray ring
-        const uint64_t idle = __ballot(L.phase == PH_IDLE);
-        if (idle && (__popcll(idle) >= TR || am == 0) && ray_tail != ray_head) {
-            const uint32_t nidle = (uint32_t)__popcll(idle);
-            const uint32_t n = ray_tail - ray_head < nidle ? ray_tail - ray_head : nidle;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint32_t rank = lane_rank(idle);
-            if (L.phase == PH_IDLE && rank < n) get_ray<VAR>(L, S.ray[w][(ray_head + rank) & kRingMask]);
-            ray_head += n;
-            lds_release(&S.ray_head[w], ray_head);
-            if (__lane_id() == 0) __hip_atomic_fetch_add(&S.events, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            progress = true;
-        }
-        if (progress) {
-            waiting = false;
-        } else {
-            if (!waiting) {
-                waiting = true;
-                t_prog = __builtin_amdgcn_s_memtime();
-            }
-            const uint32_t dn = lds_acquire(&S.done);
-            if (dn == 2u || (dn == 1u && !__ballot(L.phase != PH_IDLE))) break;
-            if (__builtin_amdgcn_s_memtime() - t_prog > RMR_SPLIT_WAIT) {
-                if (__lane_id() == 0) {
-                    lds_release(&S.done, 2u);
-                    atomicAdd(P.counters + 14, 1ull);
-                }
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (__lane_id() == 0) {
-        atomicAdd(P.counters + 0, (unsigned long long)maps);
-        atomicAdd(P.counters + 1, (unsigned long long)iters);
-#ifdef RMR_SPLIT_STATS
-        atomicAdd(P.counters + 10, (unsigned long long)cyc_starved);
-        atomicAdd(P.counters + 15, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
-#endif
-    }
-}
-
-// kernel body of a split workgroup (blockDim.x == 64 * RMR_SPLIT_WAVES). The shading role rotates
-// with the workgroup index, so the shading waves of a CU's workgroups spread over its SIMDs.
-template <int VAR, class MAP, class MATS = TableMats>
-RMR_D void trace_split(const KParams& P) {
-    static_assert(hit_in_origin<VAR, false>() && !MAP::kCache, "split kernels: HO kernels without the cache");
-    __shared__ SplitLds S;
-    if (threadIdx.x < (unsigned)kSplitMarch) {
-        S.ray_tail[threadIdx.x] = 0; S.ray_head[threadIdx.x] = 0;
-        S.hit_tail[threadIdx.x] = 0; S.hit_head[threadIdx.x] = 0;
-    }
-    if (threadIdx.x == 0) { S.done = 0; S.events = 0; }
-    __syncthreads();
-    const int wave = (int)(threadIdx.x >> 6);
-    const int shader = (int)(blockIdx.x % RMR_SPLIT_WAVES);
-    if (wave == shader) split_shade<VAR, MATS>(P, S);
-    else split_march<VAR, MAP>(P, S, wave < shader ? wave : wave - 1);
-}
 
 // Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
 RMR_D void fold_main(const KParams& P) {

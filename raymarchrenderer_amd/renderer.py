@@ -170,11 +170,6 @@ class Renderer:
         """Exact work-skipping switches (abi.CULL_*; results are bit-identical either way)."""
         _check(self._ctx, lib().rmr_set_culling(self._ctx, int(flags)))
 
-    def set_schedule(self, schedule):
-        """Wave scheduling of the specialised kernels: abi.SCHED_MEGA (every wave marches and shades)
-        (default) or abi.SCHED_SPLIT (one shading wave per seven marching waves). Bit-identical."""
-        _check(self._ctx, lib().rmr_set_schedule(self._ctx, int(schedule)))
-
     def set_stream(self, hip_stream_handle):
         _check(self._ctx, lib().rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
 

@@ -409,77 +409,10 @@ def test_scheduling_knobs_bitexact(scene):
         assert np.array_equal(imgs[0], img), k
 
 
-SPLIT_CASES = [
-    ("cornell5", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 4}, 256, 192, 8),
-    ("cornell5_sepch", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 4, "separate_channels": 1}, 96, 64, 4),
-    ("cornell5_b0", os.path.join(SCENES, "cornell5.scene"), "rm1", {"max_bounces": 0}, 40, 24, 2),
-    ("mandelbulb_b2", os.path.join(SCENES, "mandelbulb.scene"), "rm1", {"max_bounces": 2}, 128, 96, 2),
-    ("rm3_builtin", None, "rm3", {}, 128, 96, 8),
-    ("sphere1_tiny", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 1}, 7, 5, 3),
-    ("sphere1_env", os.path.join(SCENES, "sphere1.scene"), "rm1", {"max_bounces": 4, "use_env_tex": 1}, 64, 48, 4),
-    ("csg_nodes_b4", os.path.join(SCENES, "csg_nodes.scene"), "rm1", {"max_bounces": 4}, 64, 48, 4),
-]
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,path,variant,overrides,W,H,spp", SPLIT_CASES, ids=[c[0] for c in SPLIT_CASES])
-def test_split_schedule_bitexact(renderer, name, path, variant, overrides, W, H, spp):
-    """The march / shade split (rmr_set_schedule, rmr_trace.h trace_split) only moves paths between
-    lanes and waves: images and the number of map() evaluations equal the one-role schedule's."""
-    times = time_schedule(spp, frame=2)
-    out, maps = {}, {}
-    renderer.set_jit(1)
-    try:
-        for sched in (abi.SCHED_MEGA, abi.SCHED_SPLIT):
-            renderer.set_schedule(sched)
-            _setup(renderer, path, variant, W, H, overrides)
-            renderer.reset_stats()
-            renderer.render_spp(times)
-            out[sched] = renderer.read_accum()
-            st = renderer.stats()
-            assert st.jit_launches > 0
-            maps[sched] = st.map_evals
-    finally:
-        renderer.set_schedule(abi.SCHED_MEGA)
-        renderer.set_jit(2)
-    a, b = out[abi.SCHED_MEGA], out[abi.SCHED_SPLIT]
-    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
-    assert same.all(), "%s: %d values differ" % (name, (~same).sum())
-    assert maps[abi.SCHED_MEGA] == maps[abi.SCHED_SPLIT]
-    assert (maps[abi.SCHED_SPLIT] > 0) == (overrides.get("max_bounces", 16) > 0)
-
-
-@pytest.mark.gpu
-def test_split_schedule_multichunk_vs_oracle(renderer):
-    """Split kernel over 3 launches (a sample-plane budget of 2 samples) against the oracle's whole
-    image: the running mean across launches and the workgroups' rings at full occupancy."""
-    W, H = 96, 64
-    path = os.path.join(SCENES, "cornell5.scene")
-    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 4})
-    renderer.set_jit(1)
-    renderer.set_schedule(abi.SCHED_SPLIT)
-    times = time_schedule(6, frame=3)
-    try:
-        renderer.set_tuning(0, -1, W * H * 16 * 2)
-        renderer.reset_stats()
-        renderer.render_spp(times)
-        gpu = renderer.read_accum()
-        assert renderer.stats().trace_launches == 3
-    finally:
-        renderer.set_tuning(0, -1, 8 << 30)
-        renderer.set_schedule(abi.SCHED_MEGA)
-        renderer.set_jit(2)
-    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).render(times)
-    same = (gpu.view(np.uint32) == cpu.view(np.uint32)) | (np.isnan(gpu) & np.isnan(cpu))
-    assert same.all(), "%d values differ" % (~same).sum()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("step", ["0", "1"])
-def test_mandelbulb_stepped_map_bitexact_vs_oracle(renderer, monkeypatch, step):
-    """The opt-in stepped Mandelbulb map (RMR_JIT_STEP=1, rmr_trace.h MBStep: one estimator iteration
-    per lane per wave pass) and the whole-map default both equal the oracle sample for sample."""
-    monkeypatch.setenv("RMR_JIT_STEP", step)
+def test_mandelbulb_map_bitexact_vs_oracle(renderer):
+    """The specialised kernel's Mandelbulb map (mb_iter8_poly, the whole estimator per map()) equals
+    the oracle sample for sample."""
     path = os.path.join(SCENES, "mandelbulb.scene")
     W, H = 48, 40
     rect = (0, 0, W, H)
@@ -494,4 +427,4 @@ def test_mandelbulb_stepped_map_bitexact_vs_oracle(renderer, monkeypatch, step):
     cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
     a, b = gpu[..., :3], cpu[..., :3]
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
-    assert same.all(), "RMR_JIT_STEP=%s: %d samples differ" % (step, (~same.all(-1)).sum())
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()

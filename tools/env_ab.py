@@ -3,7 +3,6 @@
 trace time per setting and a bitwise comparison of the images.
 
     python tools/env_ab.py culling 7 0 [--spp 16]
-    python tools/env_ab.py schedule 1 0          (rmr_set_schedule: split / mega)
     python tools/env_ab.py shade_t 4 6 8         (rmr_set_tuning shading threshold)
     python tools/env_ab.py RMR_JIT_BAKE 1 0
 """
@@ -45,8 +44,6 @@ for name, path, variant, b in CASES:
         for v in a.values:
             if a.var == "culling":
                 r.set_culling(int(v))
-            elif a.var == "schedule":
-                r.set_schedule(int(v))
             elif a.var == "shade_t":   # shading / hand-over threshold (bits 8-15: refill threshold)
                 r.set_tuning(int(v), -1, -1)
             else:

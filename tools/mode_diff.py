@@ -1,8 +1,8 @@
 """Localise a bitwise difference between two settings of an environment switch read at scene load /
-specialisation time (e.g. RMR_SMALL_NPC 0 2): renders per-sample planes of a frame under each, lists
+specialisation time (e.g. RMR_GRID 1 0): renders per-sample planes of a frame under each, lists
 the differing samples, and runs the CPU oracle on the first few to say which setting is exact.
 
-    python tools/mode_diff.py RMR_SMALL_NPC 0 2 [--scene scenes/cornell5.scene] [--spp 4] [--bounces 4]
+    python tools/mode_diff.py RMR_GRID 1 0 [--scene scenes/cornell5.scene] [--spp 4] [--bounces 4]
     python tools/mode_diff.py culling 7 0 --scene scenes/csg256.scene    (rmr_set_culling flags)
 """
 import argparse
