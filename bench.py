@@ -483,7 +483,8 @@ def predict_partition(args, cfg):
                 load_into(fr.next_renderer(), cfg, scene_for_frame(cfg, f[0] % 120))
             fr.frame(time_schedule(nspp, frame=f[0] % 120 if animated else 0))
             f[0] += 1
-        for _ in range(max(1, args.warmup)):
+        # animated: frames 0-2 first, so that both contexts have built the live-primitive kernel
+        for _ in range(max(1, args.warmup) + (2 if animated else 0)):
             step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
