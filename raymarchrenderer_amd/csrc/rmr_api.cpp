@@ -76,7 +76,7 @@ struct rmr_ctx {
     int n_bvh = 0;
     float bvh_margin = 1e-4f;
     // candidate grid of the cache's full map() (build_grid; BVH scenes)
-    uint2* d_grid = nullptr;
+    uint4* d_grid = nullptr;
     uint16_t* d_grid_list = nullptr;
     bool grid_on = false;
     float grid_lo[3] = {0, 0, 0}, grid_inv = 1.0f, grid_sbox[6] = {0, 0, 0, 0, 0, 0};
@@ -123,7 +123,10 @@ struct rmr_ctx {
     std::vector<rmr_prim> jit_base;   // primitive values the specialised kernel was baked with
     std::vector<char> jit_live;       // primitives that moved since: loaded, not literals
     std::vector<rmr::JitKernel> jit_loaded;  // modules loaded by this context (unloaded at destroy)
-    size_t samp_budget = (size_t)8 << 30;
+    // sample planes per launch (bytes): 48 GiB, at most a quarter of the device's memory (rmr_create).
+    // 288 GB of HBM hold a whole C4 frame (3840x2160 x 256 spp: 34 GB) in one launch, so the frame
+    // pays one persistent-kernel drain instead of one per 8 GiB
+    size_t samp_budget = (size_t)48 << 30;
     std::string err;
 };
 
@@ -467,7 +470,17 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
     rmr::CandidateGrid g;
     if (!rmr::build_candidate_grid(dp, n_large, E, target, pad, g)) return RMR_OK;
     int r;
-    if ((r = dev_upload(c, &c->d_grid, (const uint2*)g.cells.data(), g.cells.size() / 2))) return r;
+    // device cells: the host record (offset | count, bound) plus the list's first four entries
+    // inline, so most full-map lanes read their candidates without a dependent list load
+    const size_t ncell = g.cells.size() / 2;
+    std::vector<uint4> cells4(ncell);
+    for (size_t i = 0; i < ncell; i++) {
+        const uint32_t x = g.cells[2 * i], off = x & 0xffffffu, cnt = x >> 24;
+        uint32_t e[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 4 && cnt != 255u && k < cnt; k++) e[k] = g.list[off + k];
+        cells4[i] = make_uint4(x, g.cells[2 * i + 1], e[0] | (e[1] << 16), e[2] | (e[3] << 16));
+    }
+    if ((r = dev_upload(c, &c->d_grid, cells4.data(), cells4.size()))) return r;
     if ((r = dev_upload(c, &c->d_grid_list, g.list.data(), g.list.size()))) return r;
     for (int k = 0; k < 3; k++) { c->grid_lo[k] = g.lo[k]; c->grid_dim[k] = g.dim[k]; }
     for (int k = 0; k < 6; k++) c->grid_sbox[k] = g.sbox[k];
@@ -827,7 +840,10 @@ int rmr_create(rmr_ctx** out, int device) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) { delete c; return RMR_E_HIP; }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+        c->n_cu = prop.multiProcessorCount;
+        if (prop.totalGlobalMem > 0) c->samp_budget = std::min(c->samp_budget, (size_t)prop.totalGlobalMem / 4);
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RMR_E_HIP; }
     c->own_stream = true;
     rmr_default_params(&c->params);

@@ -60,9 +60,10 @@ struct KParams {
     int32_t n_nodes;
     // candidate grid of the nearest-primitive cache's full map() (rmr_trace.h map_grid_npc; null =
     // none): per cell x = list offset | count << 24 (count 255: no list, take the BVH), y = float bits
-    // of a lower bound of every non-listed primitive's float distance in the cell; lists of leaf
-    // indices; leaf indices [0, grid_n_large) are evaluated everywhere (large primitives)
-    const uint2* grid;
+    // of a lower bound of every non-listed primitive's float distance in the cell, z / w = the list's
+    // first four leaf indices (16 bits each, z low first), inline; lists of leaf indices; leaf indices
+    // [0, grid_n_large) are evaluated everywhere (large primitives)
+    const uint4* grid;
     const uint16_t* grid_list;
     float grid_lo[3];
     float grid_inv;             // 1 / cell size

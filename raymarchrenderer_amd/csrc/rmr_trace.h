@@ -923,7 +923,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
     const float fz = floorf((p.z - P.grid_lo[2]) * P.grid_inv);
     bool in = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.grid_dim[0] && fy < (float)P.grid_dim[1] &&
               fz < (float)P.grid_dim[2];   // NaN: false
-    uint2 cell = make_uint2(0u, 0u);
+    uint4 cell = make_uint4(0u, 0u, 0u, 0u);
     if (in) {
         cell = P.grid[((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx];
         in = (cell.x >> 24) != 255u;
@@ -990,7 +990,14 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
             }
         }
 #endif
-        for (uint32_t i = 0; i < n; i++) {
+        // the list's first four entries are inline in the cell (no dependent load), the rest in
+        // the list; the same order either way
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const int k = (int)(((i < 2 ? cell.z : cell.w) >> (16 * (i & 1))) & 0xffffu);
+            if (i < n && k != ks) npc_insert(am_prim_at(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
+        }
+        for (uint32_t i = 4; i < n; i++) {
             const int k = (int)P.grid_list[off + i];
             if (k == ks) continue;
             npc_insert(am_prim_at(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
@@ -1880,7 +1887,7 @@ RMR_D void trace_main(const KParams& P) {
     }
     const int T = P.shade_threshold, TR = P.refill_threshold;
 #ifdef RMR_PROFILE
-    uint64_t cyc[3] = {0, 0, 0};
+    uint64_t cyc[4] = {0, 0, 0, 0};   // refill, map() iterations, shading, cache kernels: full map() batches
     const uint64_t c_begin = __builtin_amdgcn_s_memtime();
 #define RMR_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #else
@@ -2031,6 +2038,7 @@ RMR_D void trace_main(const KParams& P) {
                 const int nf = __popcll(fm), nok = __popcll(okm);
                 const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
+                    RMR_STAMP(f0);
                     if (act1 && !ok) {
                         int kw, kw2;
                         float s2;
@@ -2047,6 +2055,10 @@ RMR_D void trace_main(const KParams& P) {
                         done = true;
                     }
                     fulls++;
+#ifdef RMR_PROFILE
+                    RMR_STAMP(f1);
+                    cyc[3] += f1 - f0;
+#endif
                 }
 #ifdef RMR_NPC_CHECK   // diagnostics (RMR_JIT_OPTS=-DRMR_NPC_CHECK): every cached map() against the exact fold
                 if (done) {
@@ -2143,6 +2155,7 @@ RMR_D void trace_main(const KParams& P) {
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);
         atomicAdd(P.counters + 6, (unsigned long long)cyc[2]);
+        if (MAP::kCache) atomicAdd(P.counters + 9, (unsigned long long)cyc[3]);
         atomicAdd(P.counters + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
 #endif
     }

@@ -95,7 +95,7 @@ def test_multichunk_sample_planes_bitexact(renderer, scene, bounces):
         many = renderer.read_accum()
         assert renderer.stats().trace_launches == 4
     finally:
-        renderer.set_tuning(samp_budget=8 << 30)
+        renderer.set_tuning(samp_budget=48 << 30)   # the default (rmr_api.cpp)
         renderer.set_jit(2)
     assert _same(one, many).all()
     cpu = oracle.Oracle(scene_compile.load_scene_file(path, "rm1"), prm, view, W, H).render(times)
