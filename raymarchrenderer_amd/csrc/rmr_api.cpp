@@ -390,6 +390,7 @@ int ensure_jit(rmr_ctx* c) {
         return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
     }
     k.block = 256;
+    k.chunk = src.find("TableMap<-3>") != std::string::npos ? 64 : 128;
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
@@ -764,12 +765,14 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         P.first_sample = first_sample + k0;
         P.times = c->d_times + k0;
         P.n_units = (uint64_t)n * plane;
-        // a persistent grid no larger than the launch's work: one 128-unit chunk per wave at most
-        // (a 256x256 1-spp launch (C1) on the full grid: 0.47 ms, almost all of it waves that find
-        // no work; the per-path kernel takes one wave per 64 units as it is)
+        // a persistent grid no larger than the launch's work: one work chunk per wave at most (a
+        // 256x256 1-spp launch (C1) on the full grid: 0.47 ms, almost all of it waves that find no
+        // work; the per-path kernel takes one wave per 64 units as it is). Waves per block and units
+        // per chunk of the kernel that runs.
         int grid = full_grid;
         if (c->kernel_mode == 0 && c->grid_per_cu <= 0) {
-            const uint64_t want = (P.n_units + 4 * 128 - 1) / (4 * 128);
+            const uint64_t per_block = (uint64_t)((use_jit ? c->jit.block : 256) / 64) * (use_jit ? c->jit.chunk : 128);
+            const uint64_t want = (P.n_units + per_block - 1) / per_block;
             grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)full_grid, want));
         }
         // tuned shading batch size of the kernel that runs (measured: C2 +2% at 20; the Mandelbulb
@@ -1180,10 +1183,8 @@ int rmr_set_kernel(rmr_ctx* c, int kernel) {
     return RMR_OK;
 }
 
-// sRGB decision points of Graphics::Display's GL_FRAMEBUFFER_SRGB write: byte(c) = round(255 srgb(c))
-// for c in [0, 1] (srgb: 12.92 c below 0.0031308, else 1.055 c^(1/2.4) - 0.055), so byte(c) >= k
-// <=> srgb(c) >= (k - 1/2) / 255 <=> c >= linear((k - 1/2) / 255); out[k] is that bound rounded up to
-// a float (for a float c the comparison is then exact), out[0] = 0.
+// The candidate grid a context builds for a BVH scene, on the host (contract: rmr.h; construction:
+// grid.cpp build_candidate_grid).
 int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double target, double pad, int32_t idims[5],
                        float geom[12], uint32_t* cells, size_t cells_cap, uint16_t* list, size_t list_cap) {
     if (!prims || n <= 0 || n_large < 0 || n_large > n || !idims || !geom) return RMR_E_INVALID;
@@ -1215,6 +1216,10 @@ int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double 
     return RMR_OK;
 }
 
+// sRGB decision points of Graphics::Display's GL_FRAMEBUFFER_SRGB write: byte(c) = round(255 srgb(c))
+// for c in [0, 1] (srgb: 12.92 c below 0.0031308, else 1.055 c^(1/2.4) - 0.055), so byte(c) >= k
+// <=> srgb(c) >= (k - 1/2) / 255 <=> c >= linear((k - 1/2) / 255); out[k] is that bound rounded up to
+// a float (for a float c the comparison is then exact), out[0] = 0.
 int rmr_srgb_thresholds(float out[256]) {
     if (!out) return RMR_E_INVALID;
     out[0] = 0.0f;

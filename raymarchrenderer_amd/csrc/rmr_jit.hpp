@@ -24,6 +24,8 @@ struct JitKernel {
     int blocks_per_cu = 0;
     int shade_t = 16;           // default shading batch size for this kernel (rmr_api.cpp)
     int block = 256;            // workgroup size
+    int chunk = 128;            // units a wave takes from the work queue at a time (rmr_trace.h
+                                // RMR_CHUNK; the nearest-primitive cache kernels: RMR_CHUNK_CACHE)
 };
 
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the
