@@ -923,11 +923,10 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
     const float fz = floorf((p.z - P.grid_lo[2]) * P.grid_inv);
     bool in = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.grid_dim[0] && fy < (float)P.grid_dim[1] &&
               fz < (float)P.grid_dim[2];   // NaN: false
-    uint4 cell = make_uint4(0u, 0u, 0u, 0u);
-    if (in) {
-        cell = P.grid[((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx];
-        in = (cell.x >> 24) != 255u;
-    }
+    // the cell record is loaded without a branch (cell 0 for lanes outside the grid, unused) and
+    // first read after the large primitives' fold below, so its latency overlaps that work
+    const size_t ci = in ? ((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx : 0;
+    const uint4 cell = P.grid[ci];
     // the seed and the large primitives, every lane (approximate fold, am_*)
     float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff();
     int k1 = -1, k2 = -1;
@@ -943,6 +942,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         if (k == ks) continue;
         npc_insert(am_prim(type, p, c, r), k, u1, u2, u3, k1, k2);
     }
+    in = in && (cell.x >> 24) != 255u;   // (count 255: a cell without a list)
     // lower bound of every unlisted primitive's float distance: the cell's, or outside the grid the
     // distance to the small primitives' box (each small primitive lies in it; its float distance is
     // >= the Euclidean distance to its own box minus npc_eps) — there a lane whose seed / large minimum
