@@ -48,6 +48,10 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
 # measured on the box by tools/probes/fma_peak.hip (8 independent FMA chains per lane, 8 waves/SIMD):
 # scalar v_fma_f32 and packed v_pk_fma_f32 (the spec figure counts the packed form)
 FP32_MEASURED_TFLOPS = {"v_fma_f32": 73.8, "v_pk_fma_f32": 143.0}
+# transcendental issue limit (v_sqrt / v_exp / v_log / v_rcp ...): 8 cycles per wave64 instruction on a
+# SIMD against 4 for v_fma_f32 (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"):
+# 1024 SIMDs x 64 lanes / 8 cycles x 2.4 GHz
+TRANSC_PEAK_PER_S = 1024 * 64 / 8 * 2.4e9
 
 CONFIGS = {
     "c1": dict(scene="sphere1.scene", W=256, H=256, spp=1, bounces=1, name="C1 single-sphere SDF"),
@@ -696,6 +700,9 @@ def main():
                 "ref_equiv_achieved": round(maps_per_launch * ref_fpm / (per_launch_ms * 1e-3) / 1e12, 3),
                 "transcendentals_per_s": (round(maps_per_launch * cp["transc_per_map"] / (per_launch_ms * 1e-3), 1)
                                           if cp else None),
+                "transcendental_peak_per_s": TRANSC_PEAK_PER_S,
+                "frac_transcendental": (round(maps_per_launch * cp["transc_per_map"] / (per_launch_ms * 1e-3)
+                                              / TRANSC_PEAK_PER_S, 4) if cp else None),
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
                 "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
         if n_ctx > 1:
