@@ -676,7 +676,11 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.bvh = c->d_bvh; P.n_nodes = c->n_bvh; P.bvh_margin = c->bvh_margin;
     if (c->grid_on && c->map_np == -2) {
         P.grid = c->d_grid; P.grid_list = c->d_grid_list; P.grid_inv = c->grid_inv; P.grid_n_large = c->grid_n_large;
-        for (int k = 0; k < 3; k++) { P.grid_lo[k] = c->grid_lo[k]; P.grid_dim[k] = c->grid_dim[k]; }
+        for (int k = 0; k < 3; k++) {
+            P.grid_lo[k] = c->grid_lo[k];
+            P.grid_dim[k] = c->grid_dim[k];
+            P.grid_dimf[k] = (float)c->grid_dim[k];
+        }
         for (int k = 0; k < 6; k++) P.grid_sbox[k] = c->grid_sbox[k];
     }
     P.n_prims = (int)s.prims.size();
@@ -1332,9 +1336,14 @@ int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, 
                 if (!(code == RMR_OP_M_DIFFUSE || code == RMR_OP_M_EMISSION)) prog = true;
             }
         }
+        // the cache's primitives per lane as a context picks them (ensure_jit): one for BVH scenes,
+        // whose full map() runs through the candidate grid
+        bool simple = true;
+        for (const auto& q : s.prims) simple = simple && (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX);
+        const int npc_k = (simple && s.prims.size() > (size_t)kMaxLoopPrims) ? 1 : 2;
         std::vector<char> code;
         std::string key;
-        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog, true, 7, nullptr, false), code, key, lg);
+        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog, true, 7, nullptr, npc_k), code, key, lg);
         if (log && loglen) std::snprintf(log, loglen, "%s", ok ? key.c_str() : lg.c_str());
         return ok ? RMR_OK : RMR_E_HIP;
     } catch (const std::exception& e) {

@@ -68,6 +68,8 @@ struct KParams {
     float grid_lo[3];
     float grid_inv;             // 1 / cell size
     int32_t grid_dim[3];
+    float grid_dimf[3];         // the same as floats (the kernel's range test compares against SGPR
+                                // operands instead of converted values the allocator would spill)
     int32_t grid_n_large;
     float grid_sbox[6];         // box of the small primitives (lo.xyz, hi.xyz), rounded outward
     float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)

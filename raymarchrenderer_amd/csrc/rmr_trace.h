@@ -921,8 +921,8 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
     const float fx = floorf((p.x - P.grid_lo[0]) * P.grid_inv);
     const float fy = floorf((p.y - P.grid_lo[1]) * P.grid_inv);
     const float fz = floorf((p.z - P.grid_lo[2]) * P.grid_inv);
-    bool in = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < (float)P.grid_dim[0] && fy < (float)P.grid_dim[1] &&
-              fz < (float)P.grid_dim[2];   // NaN: false
+    bool in = fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < P.grid_dimf[0] && fy < P.grid_dimf[1] &&
+              fz < P.grid_dimf[2];   // NaN: false
     // the cell record is loaded without a branch (cell 0 for lanes outside the grid, unused) and
     // first read after the large primitives' fold below, so its latency overlaps that work
     const size_t ci = in ? ((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx : 0;
