@@ -41,3 +41,22 @@ def test_share_gpu_ranks_reduce_bitexact(gpus, config, spp):
     assert sum(p["tiles32"] for p in mg["per_rank"]) == 60 * 34
     assert mg["verify"]["bitwise_equal_to_one_context"] is True, mg["verify"]
     assert out["config"]["frame_streams"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_predict_partition_line():
+    """bench.py --predict: per-rank shares of the N-rank tile partition timed on one GPU.
+    Every rank of every N renders its own round-robin tile subset (the subsets cover the frame), and
+    the predicted speed-up is consistent with the per-rank times."""
+    out = _run("--config", "c2", "--spp", "2", "--predict", "2,4", "--steps", "2", "--warmup", "1")
+    pp = out["partition_prediction"]
+    for tile, n_tiles in (("32", 60 * 34), ("64", 30 * 17)):
+        t1 = pp["one_gpu_ms"][tile]
+        assert t1 > 0
+        for n in ("2", "4"):
+            r = pp["tiles"][tile][n]
+            assert len(r["rank_ms"]) == int(n) and sum(r["rank_tiles"]) == n_tiles
+            assert abs(r["predicted_speedup"] - t1 / max(r["rank_ms"])) < 0.01 * r["predicted_speedup"] + 1e-3
+            assert r["max_over_mean"] >= 1.0
+    assert set(pp["sample_split"]) == {"2"}   # spp 2: only N = 2 divides it
