@@ -39,7 +39,7 @@ times = time_schedule(a.spp)
 for name, path, variant, b in CASES:
     if a.scenes and name not in a.scenes.split(","):
         continue
-    res, img = {}, {}
+    res, tot, img = {}, {}, {}
     for rnd in range(a.rounds + 1):
         for v in a.values:
             if a.var == "culling":
@@ -59,8 +59,10 @@ for name, path, variant, b in CASES:
             st = r.stats()
             if rnd:
                 res.setdefault(v, []).append(st.trace_ms)
+                tot.setdefault(v, []).append(st.trace_ms + st.fold_ms)
             img[v] = r.read_accum()
     ref = img[a.values[0]].view(np.uint32)
     print(json.dumps({"scene": name, **{"%s=%s_ms" % (a.var, k): round(float(np.median(t)), 2) for k, t in res.items()},
+                      **{"%s=%s_ms_with_fold" % (a.var, k): round(float(np.median(t)), 2) for k, t in tot.items()},
                       "bitwise_equal": all(np.array_equal(ref, img[v].view(np.uint32)) for v in a.values)}), flush=True)
 r.close()
