@@ -390,7 +390,6 @@ int ensure_jit(rmr_ctx* c) {
         return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
     }
     k.block = 256;
-    if (const char* e = std::getenv("RMR_JIT_OPTS")) k.own = std::strstr(e, "-DRMR_OWN") != nullptr;
     k.chunk = src.find("TableMap<-3>") != std::string::npos ? 64 : 128;
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = 4;
@@ -766,27 +765,12 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         else if (rmr::trace_occupancy(s.variant, c->map_np, c->has_prog, &bpc) != 0 || bpc <= 0) bpc = 4;
     }
     const int full_grid = c->n_cu * bpc;
-    // pixel-owned units (RMR_OWN kernels, experiment): the first tiles are one unit per pixel; the
-    // last ~RMR_OWN_TAIL x (the grid's lanes) pixels keep per-sample units, which absorb the long
-    // tail of the pixel-owned units' nspp-sample traces
-    int own_tiles = 0;
-    if (use_jit && c->jit.own) {
-        double f = 1.0;
-        if (const char* e = std::getenv("RMR_OWN_TAIL")) f = std::max(0.0, std::atof(e));
-        const double lanes = (double)full_grid * c->jit.block;
-        const long long tail = (long long)std::ceil(f * lanes / 64.0);
-        own_tiles = (int)std::max<long long>(0, (long long)tiles.size() - tail);
-    }
-    P.own_tiles = own_tiles;
-    P.own_units = (uint32_t)own_tiles * 64u;
     for (uint32_t k0 = 0; k0 < nspp; k0 += (uint32_t)chunk) {
         const uint32_t n = (uint32_t)std::min<size_t>(chunk, nspp - k0);
         P.nspp = n;
         P.first_sample = first_sample + k0;
         P.times = c->d_times + k0;
-        P.n_units = (uint64_t)P.own_units + (uint64_t)n * (plane - P.own_units);
-        // the partial channel sums of the pixel-owned units: after the planes (<= plane x n in all)
-        P.own_part = c->d_samp + (size_t)n * (plane - P.own_units);
+        P.n_units = (uint64_t)n * plane;
         // a persistent grid no larger than the launch's work: one work chunk per wave at most (a
         // 256x256 1-spp launch (C1) on the full grid: 0.47 ms, almost all of it waves that find no
         // work; the per-path kernel takes one wave per 64 units as it is). Waves per block and units

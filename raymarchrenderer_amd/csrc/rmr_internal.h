@@ -106,12 +106,6 @@ struct KParams {
     uint64_t n_units;           // nspp * n_tiles * 64
     float4* samp;               // [nspp][n_tiles][64] per-sample radiance
     float4* accum;              // W*H running mean
-    // pixel-owned units (RMR_OWN kernels, experiment): tiles [0, own_tiles) are units of one pixel
-    // whose lane traces all nspp samples in order and folds each into accum itself (own_units =
-    // own_tiles * 64); the other tiles keep per-sample units and planes ([nspp][n_tiles - own_tiles][64])
-    int32_t own_tiles;
-    uint32_t own_units;
-    float4* own_part;           // [own_units] separateChannels partial sums of the pixel-owned units
     unsigned long long* queue;  // persistent work counter
     unsigned long long* counters; // [0] map evals, [1] samples traced
     int32_t flops_static;       // count builds (RMR_COUNT_FLOPS): flops of one map() fold without the

@@ -26,7 +26,6 @@ struct JitKernel {
     int block = 256;            // workgroup size
     int chunk = 128;            // units a wave takes from the work queue at a time (rmr_trace.h
                                 // RMR_CHUNK; the nearest-primitive cache kernels: RMR_CHUNK_CACHE)
-    bool own = false;           // built with -DRMR_OWN (pixel-owned units; experiment)
 };
 
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the

@@ -51,8 +51,7 @@ hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool p
     return hipGetLastError();
 }
 hipError_t launch_fold(const KParams& P, hipStream_t s) {
-    const uint64_t threads = (uint64_t)(P.n_tiles - P.own_tiles) * 64;   // the tiles with sample planes
-    if (threads == 0) return hipSuccess;
+    const uint64_t threads = (uint64_t)P.n_tiles * 64;
     k_fold<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(P);
     return hipGetLastError();
 }

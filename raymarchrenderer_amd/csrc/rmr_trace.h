@@ -82,9 +82,6 @@ struct Lane {
     float cs, cta;
     float texit;   // escape bound of the current ray (ray_exit)
     V3 e;          // HO kernels: the getNormal probe offset of probe ctr (normal_update cycles it)
-#ifdef RMR_OWN
-    uint32_t ks;   // pixel-owned unit: the sample being traced (0..nspp-1)
-#endif
 };
 // the first probe's offset (+h, +0, +0); the six-probe cycle of normal_update returns to it
 RMR_D void init_probe(Lane& L) { L.e = v3(0.001f, 0.0f, 0.0f); }
@@ -1156,31 +1153,12 @@ RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir, float te_pre = __bu
     return false;
 }
 
-// unit -> (sample k, pixel); false if the pixel is outside the clip rect. ks: the sample of a
-// pixel-owned unit (RMR_OWN)
-RMR_D bool unit_pixel(const KParams& P, uint32_t u, uint32_t ks, int& px, int& py, float& time) {
-#ifdef RMR_OWN
-    uint32_t k;
-    int tile, lane;
-    if (u < P.own_units) {
-        k = ks;
-        tile = (int)(u >> 6);
-        lane = (int)(u & 63u);
-    } else {
-        const uint32_t v = u - P.own_units;
-        const uint32_t per_k = (uint32_t)(P.n_tiles - P.own_tiles) * 64u;
-        k = v / per_k;
-        const uint32_t rem = v - k * per_k;
-        tile = P.own_tiles + (int)(rem >> 6);
-        lane = (int)(rem & 63u);
-    }
-#else
-    (void)ks;
+// unit -> (sample k, pixel); false if the pixel is outside the clip rect
+RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& time) {
     const uint32_t per_k = (uint32_t)P.n_tiles * 64u;
     const uint32_t k = u / per_k;
     const uint32_t rem = u - k * per_k;
     const int tile = (int)(rem >> 6), lane = (int)(rem & 63u);
-#endif
     const TileXY txy = P.tiles[tile];
     px = txy.x + (lane & 7);
     py = txy.y + (lane >> 3);
@@ -1203,43 +1181,6 @@ RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
     const V3 top = vmix(r00, r01, posx + j1 / W);
     const V3 bot = vmix(r10, r11, posx + j2 / W);
     return normalize(vmix(top, bot, posy + j3 / H));
-}
-
-// A finished sample's radiance: into its sample plane, or (pixel-owned units, RMR_OWN) folded into
-// the pixel's running mean at once, exactly as k_fold does it (RM1:600-612)
-RMR_D void emit_sample(const KParams& P, const Lane& L, float4 c) {
-#ifdef RMR_OWN
-    if (L.unit < P.own_units) {
-        const TileXY txy = P.tiles[L.unit >> 6];
-        const int px = txy.x + (int)(L.unit & 7u), py = txy.y + (int)((L.unit >> 3) & 7u);
-        float4* ap = P.accum + (size_t)py * P.W + px;
-        float4 acc = *ap;
-        const uint32_t n = P.first_sample + L.ks;
-        if (n != 0u) {
-            const float f1 = 1.0f / (float)(n + 1u);
-            const float f2 = (float)n / (float)(n + 1u);
-            acc.x = c.x * f1 + acc.x * f2;
-            acc.y = c.y * f1 + acc.y * f2;
-            acc.z = c.z * f1 + acc.z * f2;
-        } else {
-            acc.x = c.x; acc.y = c.y; acc.z = c.z;
-        }
-        acc.w = 1.0f;
-        *ap = acc;
-        return;
-    }
-    P.samp[L.unit - P.own_units] = c;
-#else
-    P.samp[L.unit] = c;
-#endif
-}
-// separateChannels: where a sample's partial channel sum waits
-RMR_D float4* partial_slot(const KParams& P, const Lane& L) {
-#ifdef RMR_OWN
-    return L.unit < P.own_units ? P.own_part + L.unit : P.samp + (L.unit - P.own_units);
-#else
-    return P.samp + L.unit;
-#endif
 }
 
 // End of trace(): store the channel result into the sample plane. Returns true when the sample
@@ -1269,24 +1210,21 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
             else if (wl < 420.0f) alpha = (wl - 380.0f) / 40.0f;
             else alpha = 1.0f;
             const V3 c = (v3(R, G, B) * alpha) * L.power;
-            emit_sample(P, L, make_float4(c.x, c.y, c.z, 1.0f));
+            P.samp[L.unit] = make_float4(c.x, c.y, c.z, 1.0f);
             return true;
         }
         if (L.chan < 0) {
-            emit_sample(P, L, make_float4(res.x, res.y, res.z, 1.0f));
+            P.samp[L.unit] = make_float4(res.x, res.y, res.z, 1.0f);
             return true;
         }
         // separateChannels: (r + g) + b, RM1:597; the partial sum lives in the sample plane
         V3 acc = res;
         if (L.chan != 0) {
-            const float4 pv = *partial_slot(P, L);
+            const float4 pv = P.samp[L.unit];
             acc = v3(pv.x, pv.y, pv.z) + res;
         }
-        if (L.chan == 2) {
-            emit_sample(P, L, make_float4(acc.x, acc.y, acc.z, 1.0f));
-            return true;
-        }
-        *partial_slot(P, L) = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        P.samp[L.unit] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        if (L.chan == 2) return true;
         L.chan++;
         L.phase = PH_RESTART;
         return false;
@@ -1315,11 +1253,7 @@ template <int VAR, bool HO>
 RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
     int px, py;
     float time, rc;
-#ifdef RMR_OWN
-    const bool in_rect = unit_pixel(P, u, L.ks, px, py, time);
-#else
-    const bool in_rect = unit_pixel(P, u, 0u, px, py, time);
-#endif
+    const bool in_rect = unit_pixel(P, u, px, py, time);
     if (fresh && !in_rect) {
         L.phase = PH_IDLE;
         return;
@@ -1355,7 +1289,7 @@ RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
     int px, py;
     float time, rc = 0.0f;
     ChunkRay r;
-    const bool in_rect = unit_pixel(P, u, 0u, px, py, time);
+    const bool in_rect = unit_pixel(P, u, px, py, time);
     V3 dir = v3s(0.0f);
     float te = __builtin_nanf("");
     if (in_rect) {
@@ -1377,9 +1311,6 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
     L.cw2 = 0;
     L.cs = -__builtin_inff();
     L.unit = u;
-#ifdef RMR_OWN
-    L.ks = 0u;
-#endif
     L.time = b.z;
     L.gxt = b.x;
     L.gyt = b.y;
@@ -1864,11 +1795,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
 // Lane state that only shading, refills and the end of a trace read (RM1 throughput / RM3 power and
 // hero wavelength, RNG chain, unit, channel, bounce count): parked in LDS, one word per lane per
 // field (conflict-free), while the nearest-primitive cache's inner march loop runs.
-#ifdef RMR_OWN
-constexpr int kColdWords = 9;
-#else
 constexpr int kColdWords = 8;
-#endif
 template <int VAR>
 RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
     s[0][t] = __uint_as_float(L.unit);
@@ -1884,9 +1811,6 @@ RMR_D void cold_put(float (*s)[256], int t, const Lane& L) {
         s[6][t] = L.color.z;
     }
     s[7][t] = __int_as_float((L.chan + 1) | (L.bounces << 8));   // chan in [-1, 2], bounces >= 0
-#ifdef RMR_OWN
-    s[8][t] = __uint_as_float(L.ks);
-#endif
 }
 template <int VAR>
 RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
@@ -1901,9 +1825,6 @@ RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
         L.color = v3(s[4][t], s[5][t], s[6][t]);
     }
     const int cb = __float_as_int(s[7][t]);
-#ifdef RMR_OWN
-    L.ks = __float_as_uint(s[8][t]);
-#endif
     L.chan = (cb & 0xff) - 1;
     L.bounces = cb >> 8;
 }
@@ -1951,9 +1872,6 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     Lane L;
     L.phase = PH_IDLE;
-#ifdef RMR_OWN
-    L.ks = 0u;
-#endif
     init_probe(L);
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
@@ -2049,8 +1967,7 @@ RMR_D void trace_main(const KParams& P) {
                 }
             }
             if (__ballot(restart)) {
-                // the next channel of this sample, or (chan -2) the next sample of a pixel-owned unit
-                if (restart) begin_trace<VAR, HO>(P, L, L.unit, L.chan == -2);
+                if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
             }
         } else if (__ballot(restart)) {
             if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
@@ -2202,14 +2119,6 @@ RMR_D void trace_main(const KParams& P) {
             if (is_shade(L.phase)) shade<VAR, PROG, MATS>(P, L);
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
-#ifdef RMR_OWN
-        // a pixel-owned unit goes on with its pixel's next sample (restarted at the next loop top)
-        if (L.phase == PH_DONE && L.unit < P.own_units && L.ks + 1u < P.nspp) {
-            L.ks++;
-            L.chan = -2;
-            L.phase = PH_RESTART;
-        }
-#endif
         if (L.phase == PH_DONE) L.phase = PH_IDLE;
 #ifdef RMR_PROFILE
         RMR_STAMP(c3);
@@ -2256,16 +2165,16 @@ RMR_D void trace_main(const KParams& P) {
 // Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
 RMR_D void fold_main(const KParams& P) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int tile = P.own_tiles + (gid >> 6), lane = gid & 63;   // (pixel-owned tiles are folded)
+    const int tile = gid >> 6, lane = gid & 63;
     if (tile >= P.n_tiles) return;
     const TileXY txy = P.tiles[tile];
     const int px = txy.x + (lane & 7), py = txy.y + (lane >> 3);
     if (px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1) return;
     float4* ap = P.accum + (size_t)py * P.W + px;
     float4 acc = *ap;
-    const size_t plane = (size_t)(P.n_tiles - P.own_tiles) * 64;
+    const size_t plane = (size_t)P.n_tiles * 64;
     for (uint32_t k = 0; k < P.nspp; k++) {
-        const float4 c = P.samp[(size_t)k * plane + (size_t)(tile - P.own_tiles) * 64 + lane];
+        const float4 c = P.samp[(size_t)k * plane + (size_t)tile * 64 + lane];
         const uint32_t n = P.first_sample + k;
         if (n != 0u) {
             const float f1 = 1.0f / (float)(n + 1u);
