@@ -107,9 +107,10 @@ def parse():
     ap.add_argument("--shade-threshold", type=int, default=0)
     ap.add_argument("--traffic-json", default="")
     ap.add_argument("--overlap", type=int, default=-1,
-                    help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU "
-                         "(measured +0.9%% at N=1; the per-launch event times then include waiting); "
-                         "0: one context; default: on for N > 1")
+                    help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU; "
+                         "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
+                         "+97%% C1, tools/overlap_ab.sh). The roofline's per-launch time then comes from "
+                         "`steps` frames rendered one at a time after the timed region")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
     ap.add_argument("--share-gpu", action="store_true",
@@ -563,9 +564,11 @@ def main():
     animated = bool(cfg.get("animated"))
 
     # overlap: two renderer contexts on two streams; consecutive frames alternate between them, so
-    # one frame's trace-kernel drain overlaps the next frame's start (multi_gpu.FrameRenderer).
-    # Default on for N > 1 (a rank's frame is 1/N as long, the drain is not).
-    overlap = args.overlap if args.overlap >= 0 else int(dist_on)
+    # one frame's trace-kernel drain (~1.2 ms of a persistent kernel's last paths on a nearly idle
+    # chip) overlaps the next frame's start (multi_gpu.FrameRenderer). Default on: a
+    # renderer producing frame after frame pipelines them; it pays most where frames are short
+    # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1).
+    overlap = args.overlap if args.overlap >= 0 else 1
     n_ctx = overlap + 1 if overlap > 0 else 1
     rs, streams = [], []
     for _ in range(n_ctx):
@@ -662,6 +665,18 @@ def main():
     value = samples / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
+    # overlapped frames: the per-launch event times include time the kernel waited behind the other
+    # context's, so the roofline's per-launch figures come from `steps` more frames rendered one at a
+    # time (each synchronised before the next starts), outside the timed region
+    if n_ctx > 1:
+        for r in rs:
+            r.reset_stats()
+        for _ in range(args.steps):
+            step()
+            fr.finish()
+            torch.cuda.synchronize()
+        st = combined_stats(rs)
+
     roof = None
     cp = None
     if rank == 0 and not args.no_count_pass and st.jit_launches:
@@ -706,7 +721,8 @@ def main():
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
                 "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
         if n_ctx > 1:
-            roof["note"] = "overlapped frames: per-launch event times include waiting for the other stream"
+            roof["note"] = ("value: %d overlapping renderer contexts; avg_launch_ms and the rates: %d frames "
+                            "rendered one at a time after the timed region" % (n_ctx, args.steps))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -60,3 +60,16 @@ def test_predict_partition_line():
             assert abs(r["predicted_speedup"] - t1 / max(r["rank_ms"])) < 0.01 * r["predicted_speedup"] + 1e-3
             assert r["max_over_mean"] >= 1.0
     assert set(pp["sample_split"]) == {"2"}   # spp 2: only N = 2 divides it
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_default_line_overlaps_frames_and_times_launches_solo():
+    """bench.py's default N = 1 line: two renderer contexts whose consecutive frames overlap (the
+    value), and the roofline's per-launch time from frames rendered one at a time afterwards."""
+    out = _run("--config", "c1", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-psnr")
+    assert out["n_gpus"] == 1 and out["config"]["frame_streams"] == 2
+    roof = out["roofline"]
+    assert "one at a time" in roof["note"]
+    assert 0 < roof["avg_launch_ms"] < 5 and roof["map_evals_per_launch"] > 0
+    assert out["value"] > 0
