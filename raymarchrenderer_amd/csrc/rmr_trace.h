@@ -1547,9 +1547,18 @@ RMR_D void run_material_v1(const KParams& P, Lane& L, int m, V3& oc, V3& od, V3&
     if (hv >= 0) oh = vf.get(hv);
 }
 // material policies of the trace kernel: table interpreter (ahead of time) or generated per scene
+RMR_D void run_material_v2(const KParams& P, Lane& L, V3 pos, V3 pdir, V3 N, V3 t0, V3 t1, V3 t2,
+                           V3& mat_color, V3& new_dir, bool& will_break);
+// Material programs from the tables (node-program interpreters); the hipRTC kernels pass generated
+// straight-line code instead (rmr_jit.cpp: JitMats for RM1 node programs, JitV2Mats for RM2's v2
+// material, whose slots then live in registers rather than a scratch array)
 struct TableMats {
     static RMR_D void run(const KParams& P, Lane& L, int m, V3& oc, V3& od, V3& oi, V3& oh) {
         run_material_v1(P, L, m, oc, od, oi, oh);
+    }
+    static RMR_D void run_v2(const KParams& P, Lane& L, V3 pos, V3 pdir, V3 N, V3 t0, V3 t1, V3 t2, V3& mat_color,
+                             V3& new_dir, bool& will_break) {
+        run_material_v2(P, L, pos, pdir, N, t0, t1, t2, mat_color, new_dir, will_break);
     }
 };
 
@@ -1598,6 +1607,19 @@ RMR_D V3 glossy_sample(Lane& L, V3 wo, V3 n, float rough) {  // material_glossy.
     det_sincos(o, so, co);
     return normalize(v3(sth * co, cth, sth * so));
 }
+// the end of the generated mat_func_<id> (Graphics.cpp:724-736): slot 1 the reflectance, slot 0
+// the new direction; shared by the interpreter below and the generated JitV2Mats
+RMR_D void v2_tail(Lane& L, V3 pos, V3 refl, V3 dir, V3& mat_color, V3& new_dir, bool& will_break) {
+    new_dir = dir;
+    const float prob = fmaxf(refl.x, fmaxf(refl.y, refl.z));
+    mat_color = L.color;
+    if (lrand(L, v2(pos.z, pos.x)) <= 1.0f) {
+        mat_color = mat_color * (refl / v3s(prob));
+        will_break = false;
+    } else {
+        will_break = true;
+    }
+}
 // generated mat_func_<id>, Graphics.cpp:705-739 + compileNode 412-463 (program is wave-uniform)
 RMR_D void run_material_v2(const KParams& P, Lane& L, V3 pos, V3 pdir, V3 N, V3 t0, V3 t1, V3 t2,
                            V3& mat_color, V3& new_dir, bool& will_break) {
@@ -1624,16 +1646,7 @@ RMR_D void run_material_v2(const KParams& P, Lane& L, V3 pos, V3 pdir, V3 N, V3 
             vf.set(ops[k].out[1], rsel);
         }
     }
-    const V3 refl = vf.get(1);
-    new_dir = vf.get(0);
-    const float prob = fmaxf(refl.x, fmaxf(refl.y, refl.z));
-    mat_color = L.color;
-    if (lrand(L, v2(pos.z, pos.x)) <= 1.0f) {
-        mat_color = mat_color * (refl / v3s(prob));
-        will_break = false;
-    } else {
-        will_break = true;
-    }
+    v2_tail(L, pos, vf.get(1), vf.get(0), mat_color, new_dir, will_break);
 }
 RMR_D V3 rm2_albedo(const KParams& P, int id) {
     if (id < 0 || id >= RMR_MAX_MATERIALS) return v3s(0.0f);
@@ -1719,7 +1732,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
                 make_tbn(N, t0, t1, t2);
                 V3 matc, nd;
                 bool wb;
-                run_material_v2(P, L, pos, pdir, N, t0, t1, t2, matc, nd, wb);
+                MATS::run_v2(P, L, pos, pdir, N, t0, t1, t2, matc, nd, wb);
                 L.color = L.color * matc;
                 if (wb) {
                     L.color = v3s(0.0f);
