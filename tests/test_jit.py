@@ -428,3 +428,58 @@ def test_mandelbulb_map_bitexact_vs_oracle(renderer):
     a, b = gpu[..., :3], cpu[..., :3]
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
+def _rm2_variant(tmp_path, name, nodes, output, constants):
+    """simple.scene's RM2 material (id 1, the built-in sphere's) with another v2 node program."""
+    import json
+    sc = {"materials": [{"id": 1, "constants": constants, "nodes": nodes, "output": output}], "objects": []}
+    p = tmp_path / (name + ".scene")
+    p.write_text(json.dumps(sc))
+    return str(p)
+
+
+# v2 programs (Graphics.cpp:405-463 compileNode) beyond simple.scene's diffuse/glossy/fresnel mix:
+# one BSDF alone, a mirror (roughness 0: reflect), and a mix whose branches are swapped
+RM2_PROGRAMS = {
+    "diffuse": ([{"name": "shader_diffuse", "inputs": [[-1, 0]]}], 0, [[0.3, 0.6, 0.9]]),
+    "glossy": ([{"name": "shader_glossy", "inputs": [[-1, 0], [-1, 1]]}], 0, [[0.9, 0.5, 0.1], 0.35]),
+    "mirror": ([{"name": "shader_glossy", "inputs": [[-1, 0], [-1, 1]]}], 0, [[1.0, 1.0, 1.0], 0.0]),
+    "mix_swapped": ([{"name": "shader_glossy", "inputs": [[-1, 1], [-1, 2]]}, {"name": "shader_diffuse", "inputs": [[-1, 0]]},
+                     {"name": "shader_mix", "inputs": [[0, 0], [1, 0], [3, 0]]}, {"name": "misc_fresnel"}], 2,
+                    [[0.2, 0.8, 0.2], [0.9, 0.9, 0.9], 0.05]),
+}
+
+
+@pytest.mark.parametrize("prog", sorted(RM2_PROGRAMS))
+def test_jit_rm2_v2_program_compiles(tmp_path, monkeypatch, prog):
+    """RM2's v2 material as generated straight-line code (JitV2Mats) compiles for every node form."""
+    nodes, out, consts = RM2_PROGRAMS[prog]
+    path = _rm2_variant(tmp_path, prog, nodes, out, consts)
+    monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path))
+    key = jit_compile_scene(path, "rm2")
+    assert (tmp_path / (key + ".hsaco")).stat().st_size > 1000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prog", sorted(RM2_PROGRAMS))
+def test_jit_rm2_v2_program_bitexact_vs_oracle(renderer, tmp_path, prog):
+    """The generated v2 material (JitV2Mats) against the oracle's table interpreter, bit for bit."""
+    nodes, out, consts = RM2_PROGRAMS[prog]
+    path = _rm2_variant(tmp_path, prog, nodes, out, consts)
+    W, H = 40, 32
+    rect = (0, 0, W, H)
+    prm, view = _setup(renderer, path, "rm2", W, H, {"max_bounces": 6})
+    renderer.set_jit(1)
+    try:
+        renderer.reset_stats()
+        times = time_schedule(3, frame=2)
+        gpu = renderer.trace_samples(times, rect)
+        st = renderer.stats()
+    finally:
+        renderer.set_jit(2)
+    assert st.jit_launches > 0
+    cpu = oracle.Oracle(_tables(path, "rm2"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%s: %d samples differ" % (prog, (~same.all(-1)).sum())
