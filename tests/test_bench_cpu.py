@@ -25,8 +25,9 @@ def _run(*args):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("gpus,config", [(2, "c2"), (3, "c5")])
+@pytest.mark.parametrize("gpus,config", [(2, "c2"), (3, "c5"), (8, "c2")])
 def test_bench_spawns_ranks_and_reduces_exactly(gpus, config):
+    """World 8 rehearses the driver's N = 8 scaling run (8 gloo ranks on the CPU, 12 tiles: uneven shares)."""
     out = _run("--gpus", str(gpus), "--dry-run", "--config", config)
     assert out["dry_run"] is True
     assert out["n_ranks"] == gpus and out["backend"] == "gloo"
