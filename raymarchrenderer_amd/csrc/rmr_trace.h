@@ -1082,7 +1082,8 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
     return v3(top.x * ib + bot.x * b, top.y * ib + bot.y * b, top.z * ib + bot.z * b);
 }
 
-// Escape bound (HO kernels of sphere/box scenes, P.esc_on). esc_boxes are boxes whose union covers
+// Escape bound (every kernel of a sphere/box/Mandelbulb scene, P.esc_on; RM2's shadow rays and the
+// node-program-material kernels since round 3). esc_boxes are boxes whose union covers
 // every primitive, each inflated by >= 0.001 + the float error of any distance at any point a march
 // reaches + the rounding of the slab parameters below (host: launch setup; 0.002 + 2^-16 (|eye| +
 // 2E + 3 maxDist)). ray_exit returns an upper bound of the last ray parameter at which the ray is
@@ -1120,8 +1121,10 @@ template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
     L.t = 0.0f;
     L.ctr = 0;
-    if (HO && phase_on_run == PH_MARCH) L.texit = (te_pre == te_pre) ? te_pre : ray_exit(P, L.o, L.d);
-    if (P.max_steps > 0 && !(HO && phase_on_run == PH_MARCH && L.texit < 0.0f)) {
+    // every march (primary, bounce, RM2's shadow rays) gets its escape bound; past it the march can
+    // only end as its miss, whose state (t = maxDist) is the same whichever step reaches it
+    L.texit = (te_pre == te_pre) ? te_pre : ray_exit(P, L.o, L.d);
+    if (P.max_steps > 0 && !(L.texit < 0.0f)) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
         L.t = P.max_dist;
@@ -1294,7 +1297,7 @@ RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
     float te = __builtin_nanf("");
     if (in_rect) {
         dir = primary_dir(P, px, py, time, rc);
-        te = HO ? ray_exit(P, v3(P.eye[0], P.eye[1], P.eye[2]), dir) : 1.0f;   // never NaN
+        te = ray_exit(P, v3(P.eye[0], P.eye[1], P.eye[2]), dir);   // never NaN
     }
     r.a = make_float4(dir.x, dir.y, dir.z, rc);
     r.b = make_float4((float)px + time, (float)py + time, time, te);
@@ -1367,7 +1370,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         L.t = fmaf(dist, P.step_mult, L.t);
         L.ctr++;
         miss = (L.ctr >= P.max_steps);
-        if (HO && !shadow) miss = miss || L.t > L.texit;   // escaped (ray_exit)
+        miss = miss || L.t > L.texit;   // escaped (ray_exit; shadow rays too)
     }
     if (miss) {
         L.t = P.max_dist;

@@ -306,16 +306,33 @@ def test_bvh_cache_nan_point_with_cached_sphere_bitexact(renderer, jit):
     assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
 
 
+def _cull_scene(scene):
+    """(path, variant) of a culling-switch case: "shelf" (NaN directions), "rm3" (built-in), "rm2:X"
+    (RM2 on golden scene X), golden scenes by name (node-program materials) or scenes/ files."""
+    if scene == "shelf":
+        return _shelf_scene(), "rm1"
+    if scene == "rm3":
+        return None, "rm3"
+    if scene.startswith("rm2:"):
+        return os.path.join(GOLDEN, "scenes", scene[4:]), "rm2"
+    g = os.path.join(GOLDEN, "scenes", scene)
+    return (g if os.path.exists(g) and not os.path.exists(os.path.join(SCENES, scene)) else os.path.join(SCENES, scene)), "rm1"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,bounces,spp", [("cornell5.scene", 4, 12), ("csg256.scene", 4, 4), ("shelf", 4, 12),
-                                               ("mandelbulb.scene", 2, 2), ("rm3", 16, 8)])
+                                               ("mandelbulb.scene", 2, 2), ("rm3", 16, 8),
+                                               ("rm2:simple.scene", 16, 8), ("default.scene", 8, 4),
+                                               ("glass_test.scene", 8, 4)])
 def test_culling_switches_bitexact(renderer, scene, bounces, spp):
     """The exact work-skipping paths (escape bound, nearest-primitive cache, approximate-then-exact
     map; rmr_set_culling) change only the number of map() calls: full renders with every switch
-    on and with every switch off are bitwise equal, on the JIT and on the table-driven kernels."""
+    on and with every switch off are bitwise equal, on the JIT and on the table-driven kernels.
+    Since round 3 the escape bound covers every kernel class: RM2 (shadow rays included) and the
+    node-program-material kernels (default, glass) as well."""
     W, H = 192, 128
-    path = _shelf_scene() if scene == "shelf" else (None if scene == "rm3" else os.path.join(SCENES, scene))
-    _setup(renderer, path, "rm3" if scene == "rm3" else "rm1", W, H, {"max_bounces": bounces})
+    path, variant = _cull_scene(scene)
+    _setup(renderer, path, variant, W, H, {"max_bounces": bounces})
     times = time_schedule(spp, frame=5)
     out, evals = {}, {}
     try:
@@ -338,13 +355,15 @@ def test_culling_switches_bitexact(renderer, scene, bounces, spp):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,W,H", [("cornell5.scene", 1920, 1080), ("csg256.scene", 960, 540)])
+@pytest.mark.parametrize("scene,W,H", [("cornell5.scene", 1920, 1080), ("csg256.scene", 960, 540),
+                                       ("rm2:simple.scene", 1920, 1080), ("default.scene", 960, 540)])
 def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
     """The same property at production frame sizes (rare events — NaN directions, near ties, cache
     bounds at grazing angles — show up only over millions of paths): every per-sample radiance of a
     2-spp frame is bitwise equal with the work-skipping paths on and off (tools/full_frame_sweep.sh
     runs the other scene families)."""
-    _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
+    path, variant = _cull_scene(scene)
+    _setup(renderer, path, variant, W, H, {"max_bounces": 4})
     times = time_schedule(2, frame=7)
     out = {}
     renderer.set_jit(1)
