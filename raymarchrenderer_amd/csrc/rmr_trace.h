@@ -1284,8 +1284,8 @@ RMR_D void begin_trace(const KParams& P, Lane& L, uint32_t u, bool fresh) {
 
 // Primary rays of a work chunk, computed full-width by the wave that fetches the chunk (instead of
 // by the few lanes each refill starts) and kept in LDS: (dir.xyz, randChange after the 3 jitter
-// rand() calls) and (gid.x + time, gid.y + time, time, escape bound of the primary ray (HO kernels;
-// 1 otherwise) or NaN outside the clip rect).
+// rand() calls) and (gid.x + time, gid.y + time, time, escape bound of the primary ray or NaN
+// outside the clip rect).
 struct ChunkRay { float4 a, b; };
 template <bool HO>
 RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
