@@ -8,6 +8,8 @@ run() { echo "== $*" >> $O; timeout -k 10 300 python tools/mode_diff.py culling 
 run --scene scenes/cornell5.scene --spp 4 --bounces 4
 run --scene tests/golden/scenes/glass_test.scene --spp 2 --bounces 16
 run --scene tests/golden/scenes/default.scene --spp 2 --bounces 16
+run --scene tests/golden/scenes/multilight.scene --spp 2 --bounces 16
+run --scene tests/golden/scenes/simple.scene --variant rm2 --spp 4 --bounces 16
 run --scene builtin --variant rm3 --spp 4 --bounces 16
 run --scene scenes/mandelbulb.scene --spp 2 --bounces 2
 run --scene scenes/csg256.scene --spp 2 --bounces 4 --W 1920 --H 1080
