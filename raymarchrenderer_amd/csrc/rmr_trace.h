@@ -1868,9 +1868,17 @@ RMR_D bool is_shade(int ph) { return ph >= PH_HIT; }   // (PH_DONE, -1, is not)
 #ifndef RMR_CACHE_WAVES
 #define RMR_CACHE_WAVES 6
 #endif
+// waves/SIMD target of the kernels with node-program materials (1 = none: the allocator's choice, 4
+// waves at ~110-120 VGPRs). Forcing 6-7 was 5-9% faster on default.scene / multilight, but the 7-wave
+// build of glass_test.scene (26 VGPRs and 40 SGPRs spilled) rendered wrong samples (sky pixels at
+// 0.8x, against the oracle), so the setting stays with the allocator (tools/env_ab.py RMR_JIT_OPTS
+// -DRMR_PROG_WAVES=N for experiments only)
+#ifndef RMR_PROG_WAVES
+#define RMR_PROG_WAVES 1
+#endif
 template <int VAR, bool GENERAL, bool PROG>
 constexpr int trace_waves() {
-    return (PROG || VAR == RMR_VARIANT_RM2) ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES);
+    return PROG ? RMR_PROG_WAVES : (VAR == RMR_VARIANT_RM2 ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES));
 }
 
 // the map() point of an active lane: one select per component in HO kernels (A/B: C2 +1%; the RM2

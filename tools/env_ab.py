@@ -30,6 +30,7 @@ G = os.path.join(ROOT, "tests", "golden", "scenes")
 CASES = [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"), "rm1", 4),
          ("multilight", os.path.join(G, "multilight.scene"), "rm1", 16),
          ("default", os.path.join(G, "default.scene"), "rm1", 16),
+         ("glass", os.path.join(G, "glass_test.scene"), "rm1", 16),
          ("rm3", None, "rm3", 16),
          ("rm2simple", os.path.join(G, "simple.scene"), "rm2", 16),
          ("csg256", os.path.join(ROOT, "scenes", "csg256.scene"), "rm1", 4),
