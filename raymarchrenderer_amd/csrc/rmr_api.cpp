@@ -79,6 +79,7 @@ struct rmr_ctx {
     uint4* d_grid = nullptr;
     uint16_t* d_grid_list = nullptr;
     bool grid_on = false;
+    bool grid_small_spheres = false;   // every primitive a cell can list is a sphere (rmr_jit.cpp)
     float grid_lo[3] = {0, 0, 0}, grid_inv = 1.0f, grid_sbox[6] = {0, 0, 0, 0, 0, 0};
     int grid_dim[3] = {0, 0, 0}, grid_n_large = 0;
     int map_np = -1;  // map() specialisation: 4/8 unrolled, 0 loop, -1 general
@@ -362,7 +363,8 @@ int ensure_jit(rmr_ctx* c) {
     // 17.4 ms per 4 spp against two); two with the BVH full map
     int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
     if (const char* e = std::getenv("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
-    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k);
+    const bool npc_spheres = c->map_np == -2 && c->grid_on && c->grid_small_spheres;
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k, npc_spheres);
     std::vector<char> code;
     std::string key, log;
     if (!rmr::jit_compile(src, code, key, log)) {
@@ -489,6 +491,9 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
     for (int k = 0; k < 6; k++) c->grid_sbox[k] = g.sbox[k];
     c->grid_inv = g.inv;
     c->grid_n_large = n_large;
+    c->grid_small_spheres = true;
+    for (size_t k = (size_t)n_large; k < dp.size(); k++)
+        c->grid_small_spheres = c->grid_small_spheres && (dp[k].type & 0xff) == RMR_PRIM_SPHERE;
     c->grid_on = true;
     return RMR_OK;
 }

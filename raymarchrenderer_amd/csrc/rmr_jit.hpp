@@ -36,8 +36,10 @@ struct JitKernel {
 // live (with bake): primitives j with live[j] != 0 are loaded even so (an animation's moving
 // primitives; the rest stay literals).
 // npc_k: primitives per lane in the nearest-primitive cache (RMR_NPC_K: 1 or 2) of BVH scenes.
+// npc_spheres: every primitive the candidate grid lists is a sphere (RMR_NPC_SPHERES: the full
+// map's candidates take the sphere distance, the same value as the general form for a sphere).
 std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
-                       const std::vector<char>* live = nullptr, int npc_k = 2);
+                       const std::vector<char>* live = nullptr, int npc_k = 2, bool npc_spheres = false);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);

@@ -914,6 +914,18 @@ RMR_D float am_prim_at(const float4* q, V3 p) {
     const V3 o = vmax0(qq);
     return (k0 + __builtin_amdgcn_sqrtf(dot(o, o))) - (box ? 0.0f : a.w);
 }
+// am_prim_at for a primitive known to be a sphere: one float4 (c.xyz, r), the sphere distance. For a
+// sphere am_prim_at computes the same value: q = |p - c| (h = 0), k0 = +0, max(q, 0) = q, and
+// |v_i| |v_i| = v_i v_i, so (0 + sqrt(len2)) - r = sqrt(len2) - r bit for bit.
+RMR_D float am_sphere_at(const float4* q, V3 p) {
+    const float4 a = q[0];
+    const V3 v = p - v3(a.x, a.y, a.z);
+    return __builtin_amdgcn_sqrtf(dot(v, v)) - a.w;
+}
+#ifndef RMR_NPC_SPHERES
+#define RMR_NPC_SPHERES 0   // 1: every primitive a grid cell lists is a sphere (rmr_jit.cpp)
+#endif
+#define RMR_AM_LISTED(q, p) (RMR_NPC_SPHERES ? am_sphere_at((q), (p)) : am_prim_at((q), (p)))
 // dtab: the leaf-ordered primitive table as float4 pairs (the LDS copy of trace_main when it has one)
 RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
                       const float4* dtab) {
@@ -995,12 +1007,12 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
             const int k = (int)(((i < 2 ? cell.z : cell.w) >> (16 * (i & 1))) & 0xffffu);
-            if (i < n && k != ks) npc_insert(am_prim_at(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
+            if (i < n && k != ks) npc_insert(RMR_AM_LISTED(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
         }
         for (uint32_t i = 4; i < n; i++) {
             const int k = (int)P.grid_list[off + i];
             if (k == ks) continue;
-            npc_insert(am_prim_at(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
+            npc_insert(RMR_AM_LISTED(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
         }
         RMR_COUNT(P.counters, active_lanes(), 12, 1);   // (the count build prices a listed primitive as a sphere)
         const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
