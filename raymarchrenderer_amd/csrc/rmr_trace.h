@@ -1114,7 +1114,9 @@ RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     float last = -__builtin_inff();
     for (int b = 0; b < P.n_esc; b++) {
-        const float* B = P.esc_boxes + 6 * b;   // wave-uniform: scalar loads
+        // wave-uniform index, constant address space: scalar loads into SGPRs (a generic pointer
+        // compiled to per-lane vector loads, one dependent L1 round trip per box)
+        CFloat* B = (CFloat*)P.esc_boxes + 6 * b;
         const float ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
         const float ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
         const float az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
