@@ -725,6 +725,10 @@ def main():
                                               / TRANSC_PEAK_PER_S, 4) if cp else None),
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
                 "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
+        if cfg.get("scene") and "mandelbulb" in str(cfg["scene"]):
+            # the stepped map (rmr_trace.h MBStep): a map() spans several wave passes, so this is
+            # map() completions per pass per lane, not the VALU lane utilisation (PMC: profiles/)
+            roof["lane_utilisation_basis"] = "map() completions per wave pass / 64 (stepped Mandelbulb map)"
         if n_ctx > 1:
             roof["note"] = ("value: %d overlapping renderer contexts; avg_launch_ms and the rates: %d frames "
                             "rendered one at a time after the timed region" % (n_ctx, args.steps))

@@ -300,6 +300,45 @@ RMR_MB_ATTR float sd_mandelbulb(V3 p, V3 c, V3 prm, unsigned long long* cnt = nu
     }
     return mb_de(r, dr);
 }
+// The same estimator one loop iteration at a time (the stepped map of the scene-specialised kernels,
+// trace_main): a lane's map() spreads over as many wave passes as its own point needs, and the rest
+// of the map() (the other primitives, the estimate, the fold, the march update) runs in batches once
+// enough lanes have finished theirs, instead of every lane waiting for the wave's slowest bailout.
+// Per lane the same operations as sd_mandelbulb's loop: mb_step runs loop iteration s.i; true when
+// the loop is over, with s.r = the final |z|.
+struct MBStep {
+    V3 z, p0;
+    float dr, r;
+    int i;
+    bool fin;   // estimator finished: waits for the next finishing batch
+};
+RMR_D void mb_begin(MBStep& s, V3 p0, int iters) {
+    s.z = p0;
+    s.p0 = p0;
+    s.dr = 1.0f;
+    s.r = 0.0f;   // (iters <= 0: the loop does not run, r stays 0)
+    s.i = 0;
+    s.fin = iters <= 0;
+}
+RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, unsigned long long* cnt) {
+    (void)cnt;
+    const V3 p0 = s.p0;
+    s.r = length(s.z);
+    if (s.r > bail) return true;
+    RMR_COUNT_MB(cnt, active_lanes(), power);
+    mb_iter(s.z, s.dr, p0, power, s.r);
+    s.i++;
+    return s.i >= iters;
+}
+// lanes finishing their estimator accumulate until RMR_MB_FIN of them (or every running lane) have
+// finished; then the rest of their map() runs once for all of them
+#ifndef RMR_MB_FIN
+#define RMR_MB_FIN 44
+#endif
+#ifndef RMR_MB_STEPPED
+#define RMR_MB_STEPPED 1   // (0: the generated stepped map's kernel runs the whole map per pass, A/B)
+#endif
+
 // Register file of a generated function (vec3 vars[total_vars]); indices are wave-uniform.
 struct VarFile {
     float x[RMR_MAX_VARS], y[RMR_MAX_VARS], z[RMR_MAX_VARS];
@@ -1043,6 +1082,7 @@ struct TableMap {
     static constexpr bool kCache = (NP == -3);
     // the map counts its own executed work (BVH traversals skip primitives; see RMR_COUNT_FLOPS)
     static constexpr bool kCounts = (NP == -2 || NP == -3);
+    static constexpr bool kStepped = false;
     static RMR_D V2 eval(const KParams& P, V3 p) {
         if constexpr (NP > 0) return map_fixed<NP>(P, p);
         else if constexpr (NP == 0) return map_loop(P, p);
@@ -1911,6 +1951,9 @@ RMR_D void trace_main(const KParams& P) {
     Lane L;
     L.phase = PH_IDLE;
     init_probe(L);
+    MBStep mbs;   // stepped map() state (MAP::kStepped); i < 0: no map() in progress
+    mbs.i = -1;
+    mbs.fin = false;
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
     WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
@@ -2124,6 +2167,39 @@ RMR_D void trace_main(const KParams& P) {
                     cold_get<VAR>(s_cold, (int)threadIdx.x, L);
                 }
             }
+        } else if constexpr (MAP::kStepped) {
+          if (amask) {
+            // stepped map() (scenes with one Mandelbulb, MBStep): every pass runs one estimator
+            // iteration for the lanes whose estimator is still running; once RMR_MB_FIN lanes have
+            // finished theirs (or none is running), those lanes complete their map() (the other
+            // primitives, the estimate and the fold: MAP::finish), apply it and begin their next one.
+            // Same operations per lane as MAP::eval, so the same bits.
+            if (is_active(L.phase) && mbs.i < 0) MAP::begin(P, RMR_MARCH_POINT(L), mbs);
+            uint32_t lmaps = 0, liters = 0;
+            for (;;) {
+                if (is_active(L.phase) && !mbs.fin) mbs.fin = MAP::step(P, mbs);
+                liters++;
+                const uint64_t fm = __ballot(is_active(L.phase) && mbs.fin);
+                const uint64_t rm = __ballot(is_active(L.phase) && !mbs.fin);
+                if (fm && (!rm || __popcll(fm) >= RMR_MB_FIN)) {
+                    if (is_active(L.phase) && mbs.fin) {
+                        if constexpr (!MAP::kCounts)
+                            RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
+                        const V2 m = MAP::finish(P, RMR_MARCH_POINT(L), mbs);
+                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                        else march_update<HO>(P, L, m);
+                        mbs.i = -1;
+                        if (is_active(L.phase)) MAP::begin(P, RMR_MARCH_POINT(L), mbs);
+                    }
+                    lmaps += (uint32_t)__popcll(fm);
+                    const uint64_t sm = __ballot(is_shade(L.phase));
+                    const uint64_t am = __ballot(is_active(L.phase));
+                    if (!am || __popcll(sm) >= T) break;
+                }
+            }
+            maps += (WCount)__builtin_amdgcn_readfirstlane(lmaps);
+            iters += (WCount)__builtin_amdgcn_readfirstlane(liters);
+          }
         } else if (amask) {
             // map() steps back to back until a shading batch is due or no lane is active: idle lanes
             // only appear in shading and refill, so the refill / restart checks can wait until then

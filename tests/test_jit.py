@@ -502,3 +502,22 @@ def test_jit_rm2_v2_program_bitexact_vs_oracle(renderer, tmp_path, prog):
     a, b = gpu[..., :3], cpu[..., :3]
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), "%s: %d samples differ" % (prog, (~same.all(-1)).sum())
+
+
+def test_jit_stepped_mandelbulb_source(tmp_path, monkeypatch):
+    """Scenes with one Mandelbulb get the stepped map (rmr_trace.h MBStep: begin / step / finish,
+    finishing batches); RMR_JIT_STEP=0 keeps the whole map per pass (another code object)."""
+    path = os.path.join(SCENES, "mandelbulb.scene")
+    monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path / "c"))
+    (tmp_path / "d").mkdir()
+    monkeypatch.setenv("RMR_JIT_DUMP", str(tmp_path / "d"))
+    k_on = jit_compile_scene(path, "rm1")
+    src = (tmp_path / "d" / (k_on + ".hip")).read_text()
+    assert "kStepped = RMR_MB_STEPPED" in src and "mb_step(s, " in src and "mb_de(s.r, s.dr)" in src
+    monkeypatch.setenv("RMR_JIT_STEP", "0")
+    k_off = jit_compile_scene(path, "rm1")
+    assert k_off != k_on
+    assert "kStepped = false" in (tmp_path / "d" / (k_off + ".hip")).read_text()
+    # a sphere/box scene has no stepped map
+    k_c5 = jit_compile_scene(os.path.join(SCENES, "cornell5.scene"), "rm1")
+    assert "kStepped = false" in (tmp_path / "d" / (k_c5 + ".hip")).read_text()
