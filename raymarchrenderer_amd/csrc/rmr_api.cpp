@@ -478,6 +478,7 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
     // device cells: the host record (offset | count, bound) plus the list's first four entries
     // inline, so most full-map lanes read their candidates without a dependent list load
     const size_t ncell = g.cells.size() / 2;
+    if (ncell >= ((size_t)1 << 31)) return RMR_OK;   // the kernel's cell index is 32-bit (map_grid_npc)
     std::vector<uint4> cells4(ncell);
     for (size_t i = 0; i < ncell; i++) {
         const uint32_t x = g.cells[2 * i], off = x & 0xffffffu, cnt = x >> 24;

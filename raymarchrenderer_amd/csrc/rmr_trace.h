@@ -976,7 +976,9 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
               fz < P.grid_dimf[2];   // NaN: false
     // the cell record is loaded without a branch (cell 0 for lanes outside the grid, unused) and
     // first read after the large primitives' fold below, so its latency overlaps that work
-    const size_t ci = in ? ((size_t)(int)fz * P.grid_dim[1] + (int)fy) * P.grid_dim[0] + (int)fx : 0;
+    // 32-bit index arithmetic: the host builds grids of fewer than 2^31 cells (build_grid)
+    const uint32_t ci = in ? ((uint32_t)fz * (uint32_t)P.grid_dim[1] + (uint32_t)fy) * (uint32_t)P.grid_dim[0] + (uint32_t)fx
+                           : 0u;
     const uint4 cell = P.grid[ci];
     // the seed and the large primitives, every lane (approximate fold, am_*)
     float u1 = __builtin_inff(), u2 = __builtin_inff(), u3 = __builtin_inff();

@@ -2,7 +2,7 @@
 # Same-process A/B of tools/librmr_base.so (tools/build_rev.sh REV tools/librmr_base.so) against the
 # working tree's librmr.so on every hot kernel class: Cornell-5 (C2), RM3 builtin, the Mandelbulb (C3),
 # csg256 (C4) and RM2 simple.scene, 1080p; bitwise comparison of the accumulators included.
-#   SPP (default 16), ROUNDS (default 6)
+#   SPP (default 16), ROUNDS (default 6), CASES (default: all five)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 S=${SPP:-16}; R=${ROUNDS:-6}
@@ -12,8 +12,10 @@ run() {   # name, ab.py args
     > "gpurun_out/ab_$n.log" 2>&1 || return $?
   echo "== $n"; cat "gpurun_out/ab_$n.log"
 }
-run c2 --spp "$S" || exit $?
-run rm3 --scene builtin --variant 3 --bounces 16 --spp "$S" || exit $?
-run c3 --scene scenes/mandelbulb.scene --bounces 2 --spp "$S" || exit $?
-run c4 --scene scenes/csg256.scene --spp 8 || exit $?
-run rm2 --scene tests/golden/scenes/simple.scene --variant 2 --bounces 16 --spp "$S" || exit $?
+C=" ${CASES:-c2 rm3 c3 c4 rm2} "   # subset, e.g. CASES="c4 c2"
+[[ $C == *" c2 "* ]] && { run c2 --spp "$S" || exit $?; }
+[[ $C == *" rm3 "* ]] && { run rm3 --scene builtin --variant 3 --bounces 16 --spp "$S" || exit $?; }
+[[ $C == *" c3 "* ]] && { run c3 --scene scenes/mandelbulb.scene --bounces 2 --spp "$S" || exit $?; }
+[[ $C == *" c4 "* ]] && { run c4 --scene scenes/csg256.scene --spp 8 || exit $?; }
+[[ $C == *" rm2 "* ]] && { run rm2 --scene tests/golden/scenes/simple.scene --variant 2 --bounces 16 --spp "$S" || exit $?; }
+exit 0
