@@ -209,10 +209,13 @@ int rmr_set_jit(rmr_ctx* ctx, int mode);
  * rmr_create:
  *   RMR_CULL_ESCAPE: a march past the exit of the inflated scene box ends as its miss
  *   RMR_CULL_NPC:    nearest-primitive cache of the BVH map (scenes of > 32 spheres/boxes)
- *   RMR_CULL_APPROX: approximate-then-exact map() of sphere/box scenes (one exact sqrt) */
+ *   RMR_CULL_APPROX: approximate-then-exact map() of sphere/box scenes (one exact sqrt)
+ *   RMR_CULL_EYE:    every primary ray's first march step is map(eye): evaluated once per wave
+ *                    (RM1 sphere/box/Mandelbulb kernels and RM3; env RMR_EYE=0 clears it) */
 #define RMR_CULL_ESCAPE 1
 #define RMR_CULL_NPC 2
 #define RMR_CULL_APPROX 4
+#define RMR_CULL_EYE 8
 int rmr_set_culling(rmr_ctx* ctx, int flags);
 /* Compile the specialised kernel of a scene without a GPU (json NULL = the variant's built-in
  * scene). On success `log` receives the code-object key, otherwise the compiler log. */

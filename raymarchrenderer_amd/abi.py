@@ -110,4 +110,5 @@ class Stats(C.Structure):
 CULL_ESCAPE = 1
 CULL_NPC = 2
 CULL_APPROX = 4
-CULL_ALL = CULL_ESCAPE | CULL_NPC | CULL_APPROX
+CULL_EYE = 8
+CULL_ALL = CULL_ESCAPE | CULL_NPC | CULL_APPROX | CULL_EYE

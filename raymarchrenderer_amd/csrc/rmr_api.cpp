@@ -109,7 +109,7 @@ struct rmr_ctx {
     // nearest-primitive cache: 40 lanes per full map() batch, or once waiting lanes >= cache-served ones
     // (R = 8; csg256 with the candidate grid: 15.7 -> 14.8 ms per 4 spp against R = 2)
     int full_threshold = 40 | (8 << 8);
-    int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX;   // rmr_set_culling
+    int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE;   // rmr_set_culling
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
@@ -727,6 +727,15 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         P.esc_boxes = c->d_esc;
         P.n_esc = (int)(c->esc_raw.size() / 6);
     }
+    {
+        // primary rays' first march step from the eye (rmr_trace.h eye_map): the march point
+        // fma(dir, 0, eye) is the eye itself for every finite direction unless an eye coordinate is
+        // -0 (then it is +-0 by the direction's sign), so that case keeps the per-lane step
+        bool neg0 = false;
+        for (int k = 0; k < 3; k++)
+            neg0 = neg0 || (c->view[k] == 0.0f && std::signbit(c->view[k])) || !std::isfinite(c->view[k]);
+        P.eye_step = (c->cull & RMR_CULL_EYE) && !neg0 ? 1 : 0;
+    }
     P.n_mats = (int)(s.variant == RMR_VARIANT_RM3 ? s.spectral.size() : s.materials.size());
     P.v2_begin = s.v2_begin; P.v2_end = s.v2_end;
     P.spec_sky = s.spectral_sky;
@@ -876,6 +885,7 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
     if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
     if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
+    if (const char* e = std::getenv("RMR_EYE")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_EYE;
     if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
@@ -1323,7 +1333,7 @@ int rmr_set_jit(rmr_ctx* c, int mode) {
 }
 
 int rmr_set_culling(rmr_ctx* c, int flags) {
-    if (!c || (flags & ~(RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX))) return RMR_E_INVALID;
+    if (!c || (flags & ~(RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE))) return RMR_E_INVALID;
     if (flags != c->cull) c->jit_ready = false;   // the specialised kernel depends on it
     c->cull = flags;
     return RMR_OK;

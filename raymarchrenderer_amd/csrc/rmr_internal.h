@@ -76,6 +76,7 @@ struct KParams {
     float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     float npc_eps0;             // nearest-primitive cache: 2^-17 E + 2^-60 (rmr_trace.h npc_eps)
     int32_t esc_on;             // escape bound (rmr_trace.h ray_exit): sphere/box scenes
+    int32_t eye_step;           // primary rays' first march step from map(eye) (rmr_trace.h eye_map)
     const float* esc_boxes;     // n_esc inflated boxes (lo.xyz, hi.xyz) covering every primitive
     int32_t n_esc;
     int32_t full_threshold;     // nearest-primitive cache: bits 0-7 lanes per full map() batch; bits 8-15 R:

@@ -1969,6 +1969,22 @@ RMR_D void trace_main(const KParams& P) {
         exhausted = true;
     }
     const int T = P.shade_threshold, TR = P.refill_threshold;
+    // eye_map: every primary ray (a fresh unit, or a separateChannels restart) starts its march at
+    // t = 0 from the eye, whose march point fma(dir, 0, eye) is the eye itself for a finite direction
+    // (the host clears P.eye_step where an eye coordinate is -0 or not finite). Its map() is therefore
+    // one value for the whole launch: evaluated here once by the wave (every lane the same point) and
+    // applied as each primary ray's first step (march_update) instead of a map() iteration. On
+    // Cornell-5 that point ties the two side walls exactly (x = 0), so it was also the approximate
+    // map's most frequent exact-fold fallback.
+    // (HO kernels: RM1 without node-program materials and RM3; the node-program-material kernels
+    // measured 0.3-1% slower with it, RM2 neutral)
+    const bool eye1 = HO && !MAP::kCache && P.eye_step != 0;
+    V2 meye = v2(0.0f, 0.0f);
+    if (eye1) {
+        meye = MAP::eval(P, v3(P.eye[0], P.eye[1], P.eye[2]));
+        meye = v2(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(meye.x))),
+                  __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(meye.y))));
+    }
 #ifdef RMR_PROFILE
     uint64_t cyc[4] = {0, 0, 0, 0};   // refill, map() iterations, shading, cache kernels: full map() batches
     const uint64_t c_begin = __builtin_amdgcn_s_memtime();
@@ -2054,6 +2070,13 @@ RMR_D void trace_main(const KParams& P) {
             }
         } else if (__ballot(restart)) {
             if (restart) begin_trace<VAR, HO>(P, L, L.unit, false);
+        }
+        if (eye1) {   // primary rays' first march step (eye_map above)
+            const float dsum = (L.d.x + L.d.y) + L.d.z;   // NaN for a NaN / infinite direction
+            const bool first = (fresh || restart) && L.phase == PH_MARCH && (dsum - dsum == 0.0f);
+            if (__ballot(first)) {
+                if (first) march_update<HO>(P, L, meye);
+            }
         }
         RMR_STAMP(c1);
         const bool act = is_active(L.phase);

@@ -242,3 +242,30 @@ def test_far_camera_bitexact(renderer, scene):
     cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
     eq = same_bits(gpu[..., :3], cpu[..., :3])
     assert eq.all(), "%d samples differ" % (~eq.all(axis=-1)).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sepch", [0, 1])
+def test_eye_first_step_switch_bitexact(renderer, sepch):
+    """RMR_CULL_EYE (rmr_trace.h eye_map): every primary ray's first march step from one map(eye)
+    per wave. Same image bit for bit with the switch on and off (separateChannels restarts too), and
+    at most one map() call fewer per primary ray (rays that escape at once never march)."""
+    W, H, spp = 64, 48, 4
+    path = os.path.join(SCENES, "cornell5.scene")
+    _setup(renderer, path, "rm1", W, H, {"max_bounces": 4, "separate_channels": sepch})
+    times = time_schedule(spp)
+    img, evals = {}, {}
+    try:
+        for flags in (abi.CULL_ALL, abi.CULL_ALL & ~abi.CULL_EYE):
+            renderer.set_culling(flags)
+            renderer.reload()
+            renderer.reset_stats()
+            renderer.render_spp(times)
+            img[flags] = renderer.read_accum()
+            evals[flags] = renderer.stats().map_evals
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+    on, off = abi.CULL_ALL, abi.CULL_ALL & ~abi.CULL_EYE
+    assert np.array_equal(img[on].view(np.uint32), img[off].view(np.uint32))
+    rays = W * H * spp * (3 if sepch else 1)
+    assert 0 < evals[off] - evals[on] <= rays

@@ -5,6 +5,8 @@ import json
 import os
 import sys
 
+import numpy as np
+
 os.environ["RMR_JIT_AMBCOUNT"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -25,7 +27,12 @@ for name, path, b in [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"
     raw = (C.c_uint64 * 16)()
     lib().rmr_get_counters(r._ctx, raw)
     out = [raw[4], raw[5]]
+    cls = {"nan_point": raw[6], "exact_tie": raw[7], "near_surface": raw[9], "l2_tiny": raw[10]}
+    f = lambda v: float(np.array([v & 0xffffffff], np.uint32).view(np.float32)[0])
+    cls["sample_tie_point"] = [f(raw[11]), f(raw[12]), f(raw[13])]
+    cls["sample_tie_dist_id"] = [f(raw[14]), f(raw[15])]
     print(json.dumps({"scene": name, "map_evals": st.map_evals, "map_iters": st.map_iters,
                       "amb_lanes": out[0], "amb_waves": out[1],
-                      "amb_lane_frac": out[0] / max(1, st.map_evals), "amb_iter_frac": out[1] / max(1, st.map_iters)}))
+                      "amb_lane_frac": out[0] / max(1, st.map_evals), "amb_iter_frac": out[1] / max(1, st.map_iters),
+                      "amb_lanes_by_class": cls}))
 r.close()
