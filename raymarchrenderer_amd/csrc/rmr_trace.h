@@ -58,6 +58,10 @@ enum Phase : int {
 //  * HO kernels (hit-in-origin: RM1 without node programs, RM3) keep the hit point in `o`: the
 //    ray origin is dead between a hit and the next bounce there. RM2 (shadow ray from the hit) and
 //    node-program materials (ray.origin is an input of shader_mix / volumeScatter) keep `hit`.
+//    In HO kernels the march does not write `o`: a finished march leaves (o, d, t), and the hit /
+//    miss point fma(d, t, o) is written to `o` when the lane enters its shading batch (one fma per
+//    component per shading event instead of an fma and a select per component in every map()
+//    iteration); the getNormal probes add their offset `e` to the same fma(d, t, o).
 struct Lane {
     uint32_t unit;
     float gxt, gyt, rc;
@@ -83,8 +87,11 @@ struct Lane {
     float texit;   // escape bound of the current ray (ray_exit)
     V3 e;          // HO kernels: the getNormal probe offset of probe ctr (normal_update cycles it)
 };
-// the first probe's offset (+h, +0, +0); the six-probe cycle of normal_update returns to it
-RMR_D void init_probe(Lane& L) { L.e = v3(0.001f, 0.0f, 0.0f); }
+// HO kernels: the march point is fma(d, t, o) + e, with e = (-0, -0, -0) while a ray marches (x + -0 = x
+// for every x, -0 and NaN included) and the probe offset from the hit on: the first probe's
+// (+h, +0, +0), set at the hit; the six-probe cycle of normal_update returns to it, and the shading
+// batch resets it to -0
+RMR_D void init_probe(Lane& L) { L.e = v3s(-0.0f); }
 template <bool HO> RMR_D V3& hitref(Lane& L) {
     if constexpr (HO) return L.o;
     else return L.hit;
@@ -1188,7 +1195,7 @@ RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre
     } else {
         L.t = P.max_dist;
         L.mid = -1.0f;
-        hitref<HO>(L) = vfma(L.d, L.t, L.o);
+        if constexpr (!HO) hitref<HO>(L) = vfma(L.d, L.t, L.o);   // (HO: written at the shading batch)
         L.phase = PH_MISS;
     }
 }
@@ -1398,10 +1405,8 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         const int cn = L.ctr + 1;
         const bool miss = !hit && (past || cn >= P.max_steps || tn > L.texit);
         const float tf = hit ? L.t : (miss ? P.max_dist : tn);
-        const bool fin = hit || miss;
-        const V3 hp = vfma(L.d, tf, L.o);
-        L.o = v3(fin ? hp.x : L.o.x, fin ? hp.y : L.o.y, fin ? hp.z : L.o.z);
-        L.t = tf;
+        L.t = tf;   // (o stays the ray origin: the shading batch writes the point, init_probe)
+        L.e = v3(hit ? 0.001f : L.e.x, hit ? 0.0f : L.e.y, hit ? 0.0f : L.e.z);
         L.mid = hit ? m.y : (miss ? -1.0f : L.mid);
         L.ctr = hit ? 0 : cn;
         L.phase = hit ? PH_NORMAL : (miss ? PH_MISS : L.phase);
@@ -1415,7 +1420,8 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         } else {
             if constexpr (CACHE) L.cs -= (L.t - L.cta) * (1.0f + 0x1p-21f);   // cache now relative to the hit
             L.mid = m.y;
-            hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            if constexpr (HO) L.e = v3(0.001f, 0.0f, 0.0f);   // first probe (init_probe)
+            else hitref<HO>(L) = vfma(L.d, L.t, L.o);
             L.ctr = 0;
             L.phase = PH_NORMAL;
         }
@@ -1434,7 +1440,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
             L.phase = PH_NEE;
         } else {
             L.mid = -1.0f;
-            hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            if constexpr (!HO) hitref<HO>(L) = vfma(L.d, L.t, L.o);
             L.phase = PH_MISS;
         }
     }
@@ -1452,15 +1458,13 @@ RMR_D V3 probe_point(const Lane& L) {
     const V3 hp = hitref<HO>(L);
     return v3(hp.x + (ax == 0 ? hs : z0), hp.y + (ax == 1 ? hs : z0), hp.z + (ax == 2 ? hs : z0));
 }
-// The map() point of an active lane without a divergent branch: march points are fma(d, t, o); a
-// probe is hit + e as fma(e, 1, hit), which is the same rounded add bit for bit (e * 1 is exact).
-// The probe offset is the lane's e (normal_update), equal to probe_point's offset for ctr.
+// The map() point of an active lane in HO kernels, without a divergent branch: fma(d, t, o) + e. A
+// marching lane has e = -0 (init_probe): its march point fma(d, t, o) exactly. A probing lane has
+// t = the hit's t, so fma(d, t, o) is the hit point, and e = probe_point's offset for ctr
+// (normal_update): hit + e, the probe.
 template <bool HO>
 RMR_D V3 march_point(const Lane& L) {
-    const bool nrm = (L.phase == PH_NORMAL);
-    const V3 D = nrm ? L.e : L.d;
-    const float T = nrm ? 1.0f : L.t;
-    return vfma(D, T, HO ? L.o : (nrm ? L.hit : L.o));
+    return vfma(L.d, L.t, L.o) + L.e;
 }
 // getNormal's differences map(p + h e_c) - map(p - h e_c) through a shift register: a + probe parks
 // its value in nrm.z; a - probe forms the difference (the same one subtraction) and, for x and y,
@@ -2255,7 +2259,13 @@ RMR_D void trace_main(const KParams& P) {
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
             shaded += (WCount)__popcll(smask);
-            if (is_shade(L.phase)) shade<VAR, PROG, MATS>(P, L);
+            if (is_shade(L.phase)) {
+                if constexpr (HO) {   // the finished march's point (init_probe); the next march's e
+                    L.o = vfma(L.d, L.t, L.o);
+                    L.e = v3s(-0.0f);
+                }
+                shade<VAR, PROG, MATS>(P, L);
+            }
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
         if (L.phase == PH_DONE) L.phase = PH_IDLE;
