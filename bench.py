@@ -278,30 +278,23 @@ def count_pass(cfg, spp, device, n_count=8):
     frame (all tiles) outside the timed region; samples are identically distributed, so the per-map
     ratios hold for the whole frame. Returns per-map executed flops, transcendentals and the
     Mandelbulb-iteration share."""
-    import ctypes as C
-    from raymarchrenderer_amd import Renderer, abi, lib, time_schedule
+    from raymarchrenderer_amd import Renderer, abi, time_schedule
     from raymarchrenderer_amd.multi_gpu import frame_tiles
     W, H = cfg["W"], cfg["H"]
     n = min(spp, n_count)
-    old = os.environ.get("RMR_JIT_OPTS")
-    os.environ["RMR_JIT_OPTS"] = ((old + " ") if old else "") + "-DRMR_COUNT_FLOPS"
     r = Renderer(device, W, H)
     try:
         r.set_jit(1)
+        r.set_instrument(abi.INSTR_COUNT_FLOPS)   # rmr_set_instrument: the counting code object
         load_into(r, cfg, scene_for_frame(cfg, 0))
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
         r.reset_stats()
         r.render_tiles(time_schedule(n), frame_tiles(W, H, TILE), TILE)
         r.sync()
-        cnt = (C.c_uint64 * 16)()
-        lib().rmr_get_counters(r.ctx, cnt)
+        cnt = r.counters()
         st = r.stats()
     finally:
         r.close()
-        if old is None:
-            os.environ.pop("RMR_JIT_OPTS", None)
-        else:
-            os.environ["RMR_JIT_OPTS"] = old
     maps = float(cnt[0])
     return {"samples": "first %d of %d samples of the frame, all tiles" % (n, spp), "map_evals": int(cnt[0]),
             "flops_per_map": cnt[11] / maps, "transc_per_map": cnt[12] / maps,
@@ -321,6 +314,7 @@ def combined_stats(rs):
     for k in ("trace_ms", "trace_launches", "map_evals", "map_iters", "jit_launches"):
         setattr(out, k, sum(getattr(x, k) for x in sts))
     out.flops_per_map = sts[0].flops_per_map
+    out.batch_maps = sum(r.counters()[14] for r in rs)   # map evals in shading batches (rmr.h counters)
     return out
 
 
@@ -683,6 +677,7 @@ def main():
         st = combined_stats(rs)
 
     roof = None
+    work_ref = None
     cp = None
     if rank == 0 and not args.no_count_pass and st.jit_launches:
         cp = count_pass(cfg, spp, local_rank)
@@ -716,15 +711,22 @@ def main():
                 "map_evals_per_launch": int(st.map_evals / st.trace_launches),
                 "flops_per_map": round(fpm, 2),
                 "flops_basis": ("executed (count pass: %s)" % cp["samples"]) if cp else "static per-map count",
-                "ref_equiv_flops_per_map": round(ref_fpm, 2),
-                "ref_equiv_achieved": round(maps_per_launch * ref_fpm / (per_launch_ms * 1e-3) / 1e12, 3),
                 "transcendentals_per_s": (round(maps_per_launch * cp["transc_per_map"] / (per_launch_ms * 1e-3), 1)
                                           if cp else None),
                 "transcendental_peak_per_s": TRANSC_PEAK_PER_S,
                 "frac_transcendental": (round(maps_per_launch * cp["transc_per_map"] / (per_launch_ms * 1e-3)
                                               / TRANSC_PEAK_PER_S, 4) if cp else None),
                 "sdf_evals_per_s": round(float(st.map_evals) / (st.trace_ms * 1e-3), 1),
-                "lane_utilisation": round(float(st.map_evals) / (64.0 * max(1, st.map_iters)), 4)}
+                # map() evaluations per map-loop lane-slot (the shading batches' certified getNormal
+                # probes are map evaluations too, outside the loop: not counted here)
+                "lane_utilisation": round(float(st.map_evals - st.batch_maps) / (64.0 * max(1, st.map_iters)), 4),
+                "map_evals_in_shading_batches": round(float(st.batch_maps) / max(1.0, float(st.map_evals)), 4)}
+        # the work a map() of the reference performs (every primitive of the scene, RM1:224-231) at the
+        # same map() rate: a measure of the work skipped, not an achieved rate (it can exceed the peak)
+        work_ref = {"flops_per_map": round(ref_fpm, 2),
+                    "equivalent_tflops": round(maps_per_launch * ref_fpm / (per_launch_ms * 1e-3) / 1e12, 3),
+                    "note": "reference-equivalent work (every primitive per map, no work skipping): not a rate "
+                            "of executed flops and not compared with the peak"}
         if cfg.get("scene") and "mandelbulb" in str(cfg["scene"]):
             # the stepped map (rmr_trace.h MBStep): a map() spans several wave passes, so this is
             # map() completions per pass per lane, not the VALU lane utilisation (PMC: profiles/)
@@ -752,7 +754,8 @@ def main():
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
                           "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world,
                           "frame_streams": n_ctx},
-               "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity}
+               "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity,
+               "reference_equivalent_work": work_ref}
         if dist_on:
             out["multi_gpu"] = {"backend": "gloo via host (--share-gpu rehearsal)" if args.share_gpu else "nccl (RCCL)",
                                 "partition": "32x32 tiles round-robin",

@@ -159,6 +159,7 @@ int rmr_reset_stats(rmr_ctx* ctx);
 int rmr_get_section_cycles(rmr_ctx* ctx, uint64_t out[4]);
 /* Raw kernel counters (diagnostics): [0] map evals, [1] map iterations, [2] shading batches,
  * [3] full map() batches of the nearest-primitive cache, [8] lanes shaded (lane-level shading events),
+ * [14] map evals in shading batches (certified getNormal probes, rmr_trace.h normal_from_prim; part of [0]),
  * [4..7] the section cycles above (or the RMR_JIT_AMBCOUNT fallback counts, tools/amb_rate.py). */
 int rmr_get_counters(rmr_ctx* ctx, uint64_t out[16]);
 /* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */
@@ -202,32 +203,40 @@ int rmr_candidate_grid(const float* prims, int n, int n_large, double E, double 
  * hipRTC for gfx950 at the first render that uses it (code objects cached in-process and under
  * $RMR_JIT_CACHE or ~/.cache/rmr-jit). Results are bit-identical to the table-driven kernels.
  * mode 0 = off, 1 = always (errors are returned), 2 = auto (default: launches of >= 2^16 units;
- * a failed compile falls back to the table-driven kernel). Env RMR_JIT overrides at rmr_create. */
+ * a failed compile falls back to the table-driven kernel). (The diagnostic build librmr_diag.so also
+ * reads env RMR_JIT at rmr_create; the release librmr.so reads no environment but RMR_JIT_CACHE.) */
 int rmr_set_jit(rmr_ctx* ctx, int mode);
 /* Exact work-skipping in the trace kernels (all results bit-identical; only the count of map()
- * calls changes), default all on; env RMR_ESC=0 / RMR_NPC=0 / RMR_JIT_APPROX=0 clear a bit at
- * rmr_create:
+ * calls changes), default all on (librmr_diag.so: env RMR_ESC=0 / RMR_NPC=0 / RMR_JIT_APPROX=0 /
+ * RMR_EYE=0 clear a bit at rmr_create):
  *   RMR_CULL_ESCAPE: a march past the exit of the inflated scene box ends as its miss
  *   RMR_CULL_NPC:    nearest-primitive cache of the BVH map (scenes of > 32 spheres/boxes)
  *   RMR_CULL_APPROX: approximate-then-exact map() of sphere/box scenes (one exact sqrt)
  *   RMR_CULL_EYE:    every primary ray's first march step is map(eye): evaluated once per wave
- *                    (RM1 sphere/box/Mandelbulb kernels and RM3; env RMR_EYE=0 clears it) */
+ *                    (RM1 sphere/box/Mandelbulb kernels and RM3) */
 #define RMR_CULL_ESCAPE 1
 #define RMR_CULL_NPC 2
 #define RMR_CULL_APPROX 4
 #define RMR_CULL_EYE 8
 int rmr_set_culling(rmr_ctx* ctx, int flags);
+/* Instrumented specialised kernels (measurement only; the images are the same bits):
+ *   RMR_INSTR_COUNT_FLOPS: the hipRTC kernel built with -DRMR_COUNT_FLOPS (rmr_trace.h count_work):
+ *     executed SDF flops / transcendentals per map() into rmr_get_counters [11] / [12] / [13], one
+ *     atomic per wave and counted event (so it is slower; bench.py's count pass, never timed).
+ * Applies to the hipRTC kernels (rmr_set_jit 1); 0 restores the production kernel. */
+#define RMR_INSTR_COUNT_FLOPS 1
+int rmr_set_instrument(rmr_ctx* ctx, int flags);
 /* Compile the specialised kernel of a scene without a GPU (json NULL = the variant's built-in
  * scene). On success `log` receives the code-object key, otherwise the compiler log. */
 int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, size_t loglen);
 /* Tuning knobs (<= 0 / < 0 keeps the current value): deferred-shading batch size in lanes (1..64),
  * persistent workgroups per CU (0 = occupancy), per-launch sample-plane budget in bytes. Until a
- * batch size is set (here or by env RMR_SHADE_T) it is chosen per kernel: 8 for general maps
+ * batch size is set (here, or by env RMR_SHADE_T in librmr_diag.so) it is chosen per kernel: 8 for general maps
  * without material programs, 16 otherwise. Results do not depend on any of these (scheduling only). */
 int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long samp_budget_bytes);
 /* (shade_threshold bits 8..15, when non-zero, set the refill threshold separately: idle lanes a
  * wave collects before it fetches new units; default (and when zero) = half the shading
- * threshold, at least 2; env RMR_REFILL_T=0 makes it the shading threshold.) */
+ * threshold, at least 2.) */
 /* Test hook: per-sample radiance (before the running mean) of the integer rect, written as
  * out[k][y-y0][x-x0][4]; sample k is seeded with times[k]. The accumulator is left unchanged. */
 int rmr_trace_samples(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out);

@@ -10,7 +10,10 @@ from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librmr.so")
-_lib = None
+# the diagnostic build (csrc/Makefile `diag`, -DRMR_DIAG=1): the same library plus the experiments'
+# environment switches (RMR_GRID, RMR_JIT_OPTS, ...), for tools/ and the A/B tests
+LIB_DIAG_PATH = os.path.join(HERE, "librmr_diag.so")
+_libs = {}
 
 EXPORTS = [
     "rmr_create", "rmr_destroy", "rmr_last_error", "rmr_build_info", "rmr_set_stream",
@@ -20,7 +23,7 @@ EXPORTS = [
     "rmr_render_spp", "rmr_render_tiles", "rmr_read_accum", "rmr_write_accum",
     "rmr_accum_device_ptr", "rmr_bind_accum", "rmr_save_bmp", "rmr_encode_bmp",
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats", "rmr_get_section_cycles", "rmr_get_counters", "rmr_set_culling",
-    "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_jit_compile_scene", "rmr_set_env_map",
+    "rmr_set_kernel", "rmr_set_tuning", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_set_instrument", "rmr_jit_compile_scene", "rmr_set_env_map",
     "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free", "rmr_display", "rmr_display_device",
     "rmr_srgb_thresholds", "rmr_candidate_grid",
 ]
@@ -37,13 +40,18 @@ def build():
     subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "csrc"), "-j8"])
 
 
-def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError("librmr.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
-                           "(expected at %s)" % LIB_PATH)
+def lib(diag=None):
+    """The ctypes handle of librmr.so, or of librmr_diag.so with diag=True. diag=None: the release
+    library unless the environment selects the diagnostic one with RMR_LIB=diag (tools/ scripts;
+    the selection is made here, in Python: the release library itself reads no such switch)."""
+    if diag is None:
+        diag = os.environ.get("RMR_LIB", "") == "diag"
+    path = LIB_DIAG_PATH if diag else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError("%s not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(expected at %s)" % (os.path.basename(path), path))
     # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, and once librmr has brought
     # in /opt/rocm's, torch can no longer initialise the GPU ("No HIP GPUs are available", measured on
     # the MI355X box). Loading torch first makes librmr bind to the runtime already in the process, so
@@ -52,7 +60,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, fp, ip = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)
     dp = C.POINTER(C.c_double)
     sig = {
@@ -92,6 +100,7 @@ def lib():
         "rmr_set_kernel": (C.c_int, [vp, C.c_int]),
         "rmr_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_longlong]),
         "rmr_set_jit": (C.c_int, [vp, C.c_int]),
+        "rmr_set_instrument": (C.c_int, [vp, C.c_int]),
         "rmr_set_env_map": (C.c_int, [vp, C.c_void_p, C.c_int, C.c_int]),
         "rmr_jit_compile_scene": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
         "rmr_trace_samples": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, fp]),
@@ -110,5 +119,5 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    _lib = L
+    _libs[path] = L
     return L

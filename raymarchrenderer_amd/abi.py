@@ -112,3 +112,5 @@ CULL_NPC = 2
 CULL_APPROX = 4
 CULL_EYE = 8
 CULL_ALL = CULL_ESCAPE | CULL_NPC | CULL_APPROX | CULL_EYE
+# rmr_set_instrument flags (rmr.h)
+INSTR_COUNT_FLOPS = 1

@@ -110,6 +110,7 @@ struct rmr_ctx {
     // (R = 8; csg256 with the candidate grid: 15.7 -> 14.8 ms per 4 spp against R = 2)
     int full_threshold = 40 | (8 << 8);
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE;   // rmr_set_culling
+    int instrument = 0;   // RMR_INSTR_* (rmr_set_instrument): instrumented specialised kernels
     int grid_per_cu = 0;  // 0 = occupancy
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
@@ -192,7 +193,7 @@ int upload_bvh(rmr_ctx* c);
 // primitives split until kMaxEscBoxes boxes). Their union covers every primitive.
 constexpr size_t kMaxEscBoxesDefault = 32;
 size_t max_esc_boxes() {   // env RMR_ESC_BOXES (experiments), read at scene upload
-    if (const char* e = std::getenv("RMR_ESC_BOXES")) return (size_t)std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = RMR_ENV("RMR_ESC_BOXES")) return (size_t)std::max(1, std::min(64, std::atoi(e)));
     return kMaxEscBoxesDefault;
 }
 // A Mandelbulb primitive (sd_mandelbulb) takes part when it iterates at least once with a bailout
@@ -267,16 +268,10 @@ void build_escape_boxes(rmr_ctx* c, bool simple) {
     }
 }
 
-int upload_scene(rmr_ctx* c) {
-    const CompiledScene& s = c->scene;
-    int r;
-    if ((r = dev_upload(c, &c->d_prims, s.prims.data(), s.prims.size()))) return r;
-    if ((r = dev_upload(c, &c->d_ops, s.ops.data(), s.ops.size()))) return r;
-    if ((r = dev_upload(c, &c->d_consts, s.consts.data(), s.consts.size()))) return r;
-    if ((r = dev_upload(c, &c->d_mats, s.materials.data(), s.materials.size()))) return r;
-    if ((r = dev_upload(c, &c->d_spec, s.spectral.data(), s.spectral.size()))) return r;
-    if ((r = dev_upload(c, &c->d_rm2, &s.rm2, 1))) return r;
-    // shading kinds (RM1): recognise the single-node diffuse / emission materials
+// Shading kinds of the RM1 materials: the single-node diffuse / emission materials run the fast
+// shading path, every other defined material its node program (has_prog). Shared by upload_scene and
+// rmr_jit_compile_scene, so both pick the same kernel class.
+std::vector<rmr::DMat> shading_kinds(const CompiledScene& s) {
     std::vector<rmr::DMat> dm(std::max<size_t>(1, s.materials.size()));
     for (size_t i = 0; i < s.materials.size(); i++) {
         const rmr_material& m = s.materials[i];
@@ -304,8 +299,25 @@ int upload_scene(rmr_ctx* c) {
         }
         dm[i] = d;
     }
-    c->has_prog = false;
-    for (const auto& d : dm) c->has_prog = c->has_prog || d.kind == rmr::MAT_PROGRAM;
+    return dm;
+}
+bool any_program(const std::vector<rmr::DMat>& dm) {
+    for (const auto& d : dm)
+        if (d.kind == rmr::MAT_PROGRAM) return true;
+    return false;
+}
+
+int upload_scene(rmr_ctx* c) {
+    const CompiledScene& s = c->scene;
+    int r;
+    if ((r = dev_upload(c, &c->d_prims, s.prims.data(), s.prims.size()))) return r;
+    if ((r = dev_upload(c, &c->d_ops, s.ops.data(), s.ops.size()))) return r;
+    if ((r = dev_upload(c, &c->d_consts, s.consts.data(), s.consts.size()))) return r;
+    if ((r = dev_upload(c, &c->d_mats, s.materials.data(), s.materials.size()))) return r;
+    if ((r = dev_upload(c, &c->d_spec, s.spectral.data(), s.spectral.size()))) return r;
+    if ((r = dev_upload(c, &c->d_rm2, &s.rm2, 1))) return r;
+    const std::vector<rmr::DMat> dm = shading_kinds(s);
+    c->has_prog = any_program(dm);
     if ((r = dev_upload(c, &c->d_dmats, dm.data(), dm.size()))) return r;
     // packed prims + map() specialisation
     bool simple = true;
@@ -332,9 +344,9 @@ int upload_scene(rmr_ctx* c) {
     }
     build_escape_boxes(c, simple);
     c->esc_infl_dev = -1.0;
-    if (const char* e = std::getenv("RMR_FULL_T"))   // (experiments; read per scene load)
+    if (const char* e = RMR_ENV("RMR_FULL_T"))   // (experiments; read per scene load)
         c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RMR_FULL_R"))
+    if (const char* e = RMR_ENV("RMR_FULL_R"))
         c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
     c->scene_loaded = true;
     c->jit_ready = false;
@@ -362,12 +374,14 @@ int ensure_jit(rmr_ctx* c) {
     // one cached primitive when the cache's full map() runs through the candidate grid (csg256: 21.5 ->
     // 17.4 ms per 4 spp against two); two with the BVH full map
     int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
-    if (const char* e = std::getenv("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
+    if (const char* e = RMR_ENV("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
     const bool npc_spheres = c->map_np == -2 && c->grid_on && c->grid_small_spheres;
     const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k, npc_spheres);
     std::vector<char> code;
     std::string key, log;
-    if (!rmr::jit_compile(src, code, key, log)) {
+    std::vector<std::string> opts;
+    if (c->instrument & RMR_INSTR_COUNT_FLOPS) opts.push_back("-DRMR_COUNT_FLOPS");
+    if (!rmr::jit_compile(src, code, key, log, opts)) {
         c->jit_failed = true;
         return fail(c, RMR_E_HIP, "hipRTC specialisation failed: " + log.substr(0, 2000));
     }
@@ -416,7 +430,7 @@ struct BvhItem {
     int idx;
 };
 int bvh_leaf_size() {   // primitives per BVH leaf (env RMR_BVH_LEAF: experiments), read at scene upload
-    if (const char* e = std::getenv("RMR_BVH_LEAF")) return std::max(1, std::min(16, std::atoi(e)));
+    if (const char* e = RMR_ENV("RMR_BVH_LEAF")) return std::max(1, std::min(16, std::atoi(e)));
     return 8;   // csg256 4 spp: 2 / 3 / 4 / 6 / 8 / 12 / 16 -> 37.0 / 36.1 / 34.1 / 33.3 / 32.9 / 33.1 / 33.6 ms
 }
 void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>& nodes, std::vector<int>& order) {
@@ -466,12 +480,12 @@ void bvh_build(std::vector<BvhItem>& it, int l, int r, std::vector<rmr::BvhNode>
 // The construction is host code (grid.cpp, build_candidate_grid); this uploads it.
 int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, double E) {
     c->grid_on = false;
-    if (const char* e = std::getenv("RMR_GRID")) if (std::atoi(e) == 0) return RMR_OK;
+    if (const char* e = RMR_ENV("RMR_GRID")) if (std::atoi(e) == 0) return RMR_OK;
     // 2^20 cells (round 3; csg256 1080p 8 spp, same process: 2^18 21.1, 2^19 20.2, 2^20 19.9 ms,
     // flat beyond; 16 MB of cell records, ~0.4 s to build on 16 host threads)
     double target = 1048576.0, pad = 0.5;
-    if (const char* e = std::getenv("RMR_GRID_CELLS")) target = std::max(1.0, std::atof(e));
-    if (const char* e = std::getenv("RMR_GRID_PAD")) pad = std::max(0.0, std::atof(e));
+    if (const char* e = RMR_ENV("RMR_GRID_CELLS")) target = std::max(1.0, std::atof(e));
+    if (const char* e = RMR_ENV("RMR_GRID_PAD")) pad = std::max(0.0, std::atof(e));
     rmr::CandidateGrid g;
     if (!rmr::build_candidate_grid(dp, n_large, E, target, pad, g)) return RMR_OK;
     int r;
@@ -499,10 +513,14 @@ int build_grid(rmr_ctx* c, const std::vector<rmr::DPrim>& dp, int n_large, doubl
     return RMR_OK;
 }
 
-int upload_bvh(rmr_ctx* c) {
-    const CompiledScene& s = c->scene;
+// Bounding boxes of a BVH scene's primitives, and which are "large": primitives much larger than the
+// typical one (ground planes, walls) would make every box above them cover the scene, so they go
+// first, in an always-visited leaf (infinite bounds), which also gives the running minimum a small
+// value early; the candidate grid lists only the others. Shared by upload_bvh and
+// rmr_jit_compile_scene (the cache kernel's RMR_NPC_SPHERES depends on the split).
+std::vector<BvhItem> bvh_items(const CompiledScene& s, std::vector<char>& is_large, float& extent) {
     std::vector<BvhItem> items;
-    float extent = 0.0f;
+    extent = 0.0f;
     for (size_t i = 0; i < s.prims.size(); i++) {
         const rmr_prim& p = s.prims[i];
         BvhItem b{};
@@ -516,16 +534,24 @@ int upload_bvh(rmr_ctx* c) {
         b.idx = (int)i;
         items.push_back(b);
     }
-    // Primitives much larger than the typical one (ground planes, walls) would make every box
-    // above them cover the scene: they go first, in an always-visited leaf (infinite bounds), which
-    // also gives the running minimum a small value early.
     std::vector<float> ext;
     for (const auto& b : items) ext.push_back(std::max({b.hi[0] - b.lo[0], b.hi[1] - b.lo[1], b.hi[2] - b.lo[2]}));
     std::vector<float> sorted_ext = ext;
+    is_large.assign(items.size(), 0);
+    if (items.empty()) return items;
     std::nth_element(sorted_ext.begin(), sorted_ext.begin() + sorted_ext.size() / 2, sorted_ext.end());
     const float big = 8.0f * sorted_ext[sorted_ext.size() / 2];
+    for (size_t i = 0; i < items.size(); i++) is_large[i] = ext[i] > big;
+    return items;
+}
+
+int upload_bvh(rmr_ctx* c) {
+    const CompiledScene& s = c->scene;
+    std::vector<char> is_large;
+    float extent = 0.0f;
+    const std::vector<BvhItem> items = bvh_items(s, is_large, extent);
     std::vector<BvhItem> small, large;
-    for (size_t i = 0; i < items.size(); i++) (ext[i] > big ? large : small).push_back(items[i]);
+    for (size_t i = 0; i < items.size(); i++) (is_large[i] ? large : small).push_back(items[i]);
     std::vector<rmr::BvhNode> nodes;
     std::vector<int> order;
     if (!large.empty()) {
@@ -877,17 +903,17 @@ int rmr_create(rmr_ctx** out, int device) {
         rmr_destroy(c);
         return RMR_E_HIP;
     }
-    if (const char* e = std::getenv("RMR_SHADE_T")) {
+    if (const char* e = RMR_ENV("RMR_SHADE_T")) {
         c->shade_threshold = std::max(1, std::atoi(e));
         c->shade_auto = false;
     }
-    if (const char* e = std::getenv("RMR_REFILL_T")) c->refill_threshold = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
-    if (const char* e = std::getenv("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
-    if (const char* e = std::getenv("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
-    if (const char* e = std::getenv("RMR_EYE")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_EYE;
-    if (const char* e = std::getenv("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = RMR_ENV("RMR_REFILL_T")) c->refill_threshold = std::max(0, std::atoi(e));
+    if (const char* e = RMR_ENV("RMR_ESC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_ESCAPE;
+    if (const char* e = RMR_ENV("RMR_NPC")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_NPC;
+    if (const char* e = RMR_ENV("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
+    if (const char* e = RMR_ENV("RMR_EYE")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_EYE;
+    if (const char* e = RMR_ENV("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
+    if (const char* e = RMR_ENV("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
     *out = c;
     return RMR_OK;
@@ -1343,29 +1369,44 @@ int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, 
     std::string lg;
     try {
         CompiledScene s = (json && len) ? rmr::compile_scene(std::string(json, len), variant) : rmr::builtin_scene(variant);
-        bool prog = false;  // same rule as upload_scene: any RM1 material that is not a fast kind
-        if (s.variant == RMR_VARIANT_RM1) {
-            for (const auto& m : s.materials) {
-                if (!m.defined) continue;
-                const bool single = m.prog_end - m.prog_begin == 1 && m.inside_var < 0 && m.hit_var < 0;
-                const int code = single ? s.ops[(size_t)m.prog_begin].code : -1;
-                if (!(code == RMR_OP_M_DIFFUSE || code == RMR_OP_M_EMISSION)) prog = true;
-            }
-        }
-        // the cache's primitives per lane as a context picks them (ensure_jit): one for BVH scenes,
-        // whose full map() runs through the candidate grid
+        // the kernel class as a context picks it: node-program materials by upload_scene's rule
+        // (shading_kinds), the cache's primitives per lane and the sphere-only candidates as
+        // ensure_jit for BVH scenes, whose full map() runs through the candidate grid (assumed built,
+        // as it is unless the grid would exceed 2^31 cells)
+        const bool prog = any_program(shading_kinds(s));
         bool simple = true;
         for (const auto& q : s.prims) simple = simple && (q.type == RMR_PRIM_SPHERE || q.type == RMR_PRIM_BOX);
-        const int npc_k = (simple && s.prims.size() > (size_t)kMaxLoopPrims) ? 1 : 2;
+        const bool bvh = simple && s.prims.size() > (size_t)kMaxLoopPrims;
+        bool npc_spheres = bvh;
+        if (bvh) {
+            std::vector<char> is_large;
+            float extent = 0.0f;
+            (void)bvh_items(s, is_large, extent);
+            for (size_t i = 0; i < s.prims.size(); i++)
+                npc_spheres = npc_spheres && (is_large[i] || s.prims[i].type == RMR_PRIM_SPHERE);
+        }
         std::vector<char> code;
         std::string key;
-        const bool ok = rmr::jit_compile(rmr::jit_source(s, prog, true, 7, nullptr, npc_k), code, key, lg);
+        const bool ok = rmr::jit_compile(
+            rmr::jit_source(s, prog, true, RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE, nullptr,
+                            bvh ? 1 : 2, npc_spheres),
+            code, key, lg);
         if (log && loglen) std::snprintf(log, loglen, "%s", ok ? key.c_str() : lg.c_str());
         return ok ? RMR_OK : RMR_E_HIP;
     } catch (const std::exception& e) {
         if (log && loglen) std::snprintf(log, loglen, "%s", e.what());
         return RMR_E_SCENE;
     }
+}
+
+int rmr_set_instrument(rmr_ctx* c, int flags) {
+    if (!c || (flags & ~RMR_INSTR_COUNT_FLOPS)) return RMR_E_INVALID;
+    if (flags != c->instrument) {
+        c->instrument = flags;
+        c->jit_ready = false;   // another code object (its own cache key)
+        c->jit_failed = false;
+    }
+    return RMR_OK;
 }
 
 int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long samp_budget_bytes) {

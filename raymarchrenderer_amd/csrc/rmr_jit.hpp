@@ -15,6 +15,20 @@
 
 #include "scene.hpp"
 
+// Environment switches (RMR_GRID, RMR_JIT_OPTS, RMR_JIT_BAKE, ...: A/B experiments, tools/) exist only
+// in the diagnostic build librmr_diag.so (`make diag`, -DRMR_DIAG=1). The release librmr.so reads no
+// environment variable but RMR_JIT_CACHE (and HOME for its default): a drop-in renderer's results and
+// kernels do not depend on an inherited environment. RMR_ENV("X") is nullptr there, and the name
+// does not reach the binary.
+#ifndef RMR_DIAG
+#define RMR_DIAG 0
+#endif
+#if RMR_DIAG
+#define RMR_ENV(name) std::getenv(name)
+#else
+#define RMR_ENV(name) ((const char*)nullptr)
+#endif
+
 namespace rmr {
 
 struct JitKernel {
@@ -42,6 +56,9 @@ std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int 
                        const std::vector<char>* live = nullptr, int npc_k = 2, bool npc_spheres = false);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
-bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log);
+// opts: further compiler options, part of the key (the instrumented build of rmr_set_instrument:
+// -DRMR_COUNT_FLOPS).
+bool jit_compile(const std::string& src, std::vector<char>& code, std::string& key, std::string& log,
+                 const std::vector<std::string>& opts = {});
 
 }  // namespace rmr

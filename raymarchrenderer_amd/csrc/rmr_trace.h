@@ -560,6 +560,37 @@ RMR_D V2 am_result(const KParams& P, const AMin& m) {
     return d;
 }
 
+// ---- getNormal from one primitive (HO sphere/box kernels with the approximate map) ----------------
+// The generated approximate map (rmr_jit.cpp) can carry each primitive's scene index j (< 256) in the
+// low 8 mantissa bits of its material-id literal: ids are integer-valued floats of magnitude < 2^15,
+// whose low 9 mantissa bits are zero, so the fold's selects move (id | j) and am_id_of recovers the id
+// bit for bit (0 | j is a denormal pattern, & ~0xff gives +0 back; -1 keeps its bits). The minimiser's
+// index w = am_w_of then names the primitive the hit is on.
+RMR_D float am_pack(float id, int j) { return __int_as_float(__float_as_int(id) | j); }
+RMR_D float am_id_of(float packed) { return __int_as_float(__float_as_int(packed) & ~0xff); }
+RMR_D int am_w_of(float packed) { return __float_as_int(packed) & 0xff; }
+RMR_D V2 am_result_packed(const KParams& P, const AMin& m) {
+    V2 d = v2(P.max_dist, -1.0f);
+    opu(d, sqrt_cr_big(m.l2) + m.k, am_id_of(m.id));
+    return d;
+}
+#define NPC_PROBE_DELTA 0.0010001f
+// Certificate, at a march point p, that getNormal's six probes p +- h e_c (RM1:259-268) all have w as
+// the unique minimiser of the opU fold, so each probe's map() is opU((maxDist, -1), F_w(probe), id_w)
+// (the fold's closed form, map_bvh) and its distance is primitive w's alone. With eps = npc_eps over
+// the probes' box (float evaluation error of any box/sphere distance, 4x slack; npc_eps below) and
+// delta = NPC_PROBE_DELTA >= |probe - p|, SDFs being 1-Lipschitz:
+//   F_w(probe) <= a + err(a) + 2 eps + delta,   F_j(probe) >= s2 - err(s2) - 2 eps - delta  (j != w),
+// a / s2 the approximate minimum / runner-up (am_*: |a_j - F_j| <= err(a_j) = 2^-21 (|a_j| + R) +
+// 2^-40, monotonic in a_j). So s2 - a > err(a) + err(s2) + 4 eps + 2 delta suffices; the test below
+// takes am_unique's doubled margin and |s2| + |a| 2^-20 for its own rounding. NaN: false.
+RMR_D bool am_normal_cert(const KParams& P, const AMin& m, V3 p, float R2) {
+    const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
+    const float eps = fmaf(ax + 0.002f, 0x1p-17f, P.npc_eps0);
+    const float margin = fmaf(fabsf(m.a) + fabsf(m.s2) + R2, 0x1p-20f, 0x1p-39f);
+    return m.s2 - m.a > fmaf(4.0f, eps, margin + 2.0f * NPC_PROBE_DELTA);
+}
+
 // One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
 // in flight while prim j is evaluated (A/B: +2% over loading at use). The IEEE sqrt sequence hipcc
 // is replaced by rmr::sqrt_cr (same bits, 6 fewer VALU per sqrt; rmr_math.h).
@@ -689,7 +720,6 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
     const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
     return fmaf(ax, 0x1p-17f, P.npc_eps0);
 }
-#define NPC_PROBE_DELTA 0.0010001f
 #define NPC_BOUNCE_DELTA 0.0031f
 // exact distance of leaf-order primitive k at p, bit-identical to sd_box / sd_sphere at points
 // without NaN: a sphere is the box of half-extent 0 (|v| - 0 = |v|, max(|v|, 0) = |v|, dot(|v|,|v|) =
@@ -1089,6 +1119,13 @@ template <int NP>
 struct TableMap {
     // NP == -3: the BVH map with the nearest-primitive cache (trace_main's kCache path)
     static constexpr bool kCache = (NP == -3);
+    // eval_c certifies the hit primitive's getNormal probes (am_normal_cert; generated maps only)
+    static constexpr bool kCert = false;
+    static RMR_D V2 eval_c(const KParams& P, V3 p, int& w, bool& cert) {
+        w = 0;
+        cert = false;
+        return eval(P, p);
+    }
     // the map counts its own executed work (BVH traversals skip primitives; see RMR_COUNT_FLOPS)
     static constexpr bool kCounts = (NP == -2 || NP == -3);
     static constexpr bool kStepped = false;
@@ -1184,9 +1221,13 @@ template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
     L.t = 0.0f;
     L.ctr = 0;
-    // every march (primary, bounce, RM2's shadow rays) gets its escape bound; past it the march can
-    // only end as its miss, whose state (t = maxDist) is the same whichever step reaches it
-    L.texit = (te_pre == te_pre) ? te_pre : ray_exit(P, L.o, L.d);
+    // every march from outside (primary, bounce, RM2's shadow rays) gets its escape bound; past it
+    // the march can only end as its miss, whose state (t = maxDist) is the same whichever step
+    // reaches it. An inside march (distMult = -1, RM1:498-505) does not: past its object's box the
+    // reference's next map() is positive, -map < 0.001, a hit — which a step longer than the distance
+    // to the surface (stepMultiply > 1) can reach in one step from inside
+    const bool inside_march = L.inside && phase_on_run != PH_SHADOW;
+    L.texit = (te_pre == te_pre) ? te_pre : (inside_march ? __builtin_inff() : ray_exit(P, L.o, L.d));
     if (P.max_steps > 0 && !(L.texit < 0.0f)) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
@@ -1394,8 +1435,12 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 
 // one map() result applied to a lane in PH_MARCH / PH_SHADOW (march(), RM1:233-257)
 // distMult = inside ? -1 : 1 (RM1:498-505); m.x * -1.0f == -m.x exactly. Shadow rays use +1.
+// cert / w (HO kernels whose map certifies its minimiser, MAP::kCert): a hit whose getNormal probes
+// all have primitive w as their unique minimiser (am_normal_cert) skips the six probe iterations: it
+// parks in PH_HIT with ctr = -1, and the shading batch evaluates the probes on w alone
+// (normal_from_prim), the same six map() values
 template <bool HO, bool CACHE = false>
-RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
+RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = false) {
     if constexpr (HO && !CACHE) {   // (cache kernels: A/B neutral-negative)
         // HO kernels (no shadow rays): the same state transitions as below as per-lane selects
         const float dist = L.inside ? -m.x : m.x;
@@ -1405,11 +1450,13 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m) {
         const int cn = L.ctr + 1;
         const bool miss = !hit && (past || cn >= P.max_steps || tn > L.texit);
         const float tf = hit ? L.t : (miss ? P.max_dist : tn);
+        const bool probe = hit && !cert;
         L.t = tf;   // (o stays the ray origin: the shading batch writes the point, init_probe)
-        L.e = v3(hit ? 0.001f : L.e.x, hit ? 0.0f : L.e.y, hit ? 0.0f : L.e.z);
+        L.e = v3(probe ? 0.001f : L.e.x, probe ? 0.0f : L.e.y, probe ? 0.0f : L.e.z);
         L.mid = hit ? m.y : (miss ? -1.0f : L.mid);
-        L.ctr = hit ? 0 : cn;
-        L.phase = hit ? PH_NORMAL : (miss ? PH_MISS : L.phase);
+        L.ctr = hit ? (cert ? -1 : 0) : cn;
+        L.phase = hit ? (cert ? PH_HIT : PH_NORMAL) : (miss ? PH_MISS : L.phase);
+        L.cw = cert ? w : L.cw;
         return;
     }
     const bool shadow = (L.phase == PH_SHADOW);
@@ -1484,6 +1531,29 @@ RMR_D void normal_update(Lane& L, float m) {
     L.e = plus ? -L.e : v3(-L.e.z, -L.e.x, -L.e.y);
     L.ctr++;
     if (L.ctr == 6) L.phase = PH_HIT;   // normalize() happens in the shading batch (shade())
+}
+
+// getNormal (RM1:259-268) of a hit certified by its march_update (cert, w): the six probes hp + e_c
+// with normal_update's offsets and signed zeros, each probe's map() = opU((maxDist, -1), F_w(probe),
+// id_w) whose distance is F_w (or maxDist beyond it); F_w by prim_dist_at, bit-identical to sd_box /
+// sd_sphere at points without NaN (the hit point is finite: am_normal_cert). One per-lane table read
+// of the primitive for the six.
+RMR_D V3 normal_from_prim(const KParams& P, V3 hp, int w) {
+    const float4* q = (const float4*)(P.dprims + w);
+    const float4 qa = q[0], qb = q[1];
+    const float4 pr[2] = {qa, qb};
+    const float h = 0.001f;
+    float mv[6];
+    V3 e = v3(h, 0.0f, 0.0f);
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        float mid;
+        int j;
+        const float F = prim_dist_at(pr, hp + e, mid, j);
+        mv[c] = (P.max_dist >= F) ? F : P.max_dist;   // opu(d = (maxDist, -1), F, .).x
+        e = (c & 1) == 0 ? -e : v3(-e.z, -e.x, -e.y);   // normal_update's cycle
+    }
+    return v3(mv[0] - mv[1], mv[2] - mv[3], mv[4] - mv[5]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1737,9 +1807,13 @@ RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) 
 // ------------------------------------------------------------------------------------------
 // shading of the parked lanes
 // ------------------------------------------------------------------------------------------
-template <int VAR, bool PROG, class MATS>
+template <int VAR, bool PROG, class MATS, bool CERT = false>
 RMR_D void shade(const KParams& P, Lane& L) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
+    // certified hits (march_update cert, ctr = -1): getNormal's probes on the hit's primitive alone
+    if constexpr (HO && CERT) {
+        if (L.phase == PH_HIT && L.ctr < 0) L.nrm = normal_from_prim(P, hitref<HO>(L), L.cw);
+    }
     // getNormal's normalize (RM1:267), deferred from the last probe to the batch: the map loop then
     // carries no division/sqrt for the few lanes that finish a normal in a given iteration
     if (L.phase == PH_HIT) L.nrm = normalize(L.nrm);
@@ -1962,7 +2036,7 @@ RMR_D void trace_main(const KParams& P) {
     mbs.fin = false;
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
-    WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0;
+    WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, bmaps = 0;
     constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
@@ -2240,9 +2314,17 @@ RMR_D void trace_main(const KParams& P) {
                     const V3 p = RMR_MARCH_POINT(L);
                     if constexpr (!MAP::kCounts)   // every primitive of the fold (Mandelbulb iterations: inside)
                         RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);
-                    const V2 m = MAP::eval(P, p);
-                    if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                    else march_update<HO>(P, L, m);
+                    if constexpr (MAP::kCert && HO) {
+                        int w;
+                        bool cert;
+                        const V2 m = MAP::eval_c(P, p, w, cert);
+                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                        else march_update<HO>(P, L, m, w, cert);
+                    } else {
+                        const V2 m = MAP::eval(P, p);
+                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                        else march_update<HO>(P, L, m);
+                    }
                 }
                 lmaps += (uint32_t)__popcll(am);
                 liters++;
@@ -2259,12 +2341,23 @@ RMR_D void trace_main(const KParams& P) {
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
             shaded += (WCount)__popcll(smask);
+            if constexpr (MAP::kCert && HO) {   // the certified hits' probes (shade: normal_from_prim)
+                const uint64_t cm = __ballot(L.phase == PH_HIT && L.ctr < 0);
+                maps += (WCount)(6 * __popcll(cm));
+                bmaps += (WCount)(6 * __popcll(cm));
+#ifdef RMR_COUNT_FLOPS
+                const uint64_t bm = __ballot(L.phase == PH_HIT && L.ctr < 0 &&
+                                             (__float_as_int(((const float4*)(P.dprims + L.cw))[1].z) & 0xff) == RMR_PRIM_BOX);
+                RMR_COUNT(P.counters, (uint64_t)__popcll(bm), 6 * (22 + 2), 6);
+                RMR_COUNT(P.counters, (uint64_t)__popcll(cm & ~bm), 6 * (10 + 2), 6);
+#endif
+            }
             if (is_shade(L.phase)) {
                 if constexpr (HO) {   // the finished march's point (init_probe); the next march's e
                     L.o = vfma(L.d, L.t, L.o);
                     L.e = v3s(-0.0f);
                 }
-                shade<VAR, PROG, MATS>(P, L);
+                shade<VAR, PROG, MATS, MAP::kCert && HO>(P, L);
             }
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
@@ -2286,8 +2379,10 @@ RMR_D void trace_main(const KParams& P) {
                 atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
                 if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
                 atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
+                // map() evaluations of the shading batches (certified getNormal probes; in [0] too)
+                if (MAP::kCert && HO) atomicAdd(P.counters + 14, (unsigned long long)bmaps);
             }
-            maps = iters = shades = fulls = shaded = 0;
+            maps = iters = shades = fulls = shaded = bmaps = 0;
         }
         if (last) break;
     }

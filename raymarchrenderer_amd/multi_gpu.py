@@ -30,14 +30,15 @@ def tile_partition(W, H, tile, rank, world):
     return np.array(t[rank::world], np.int32).reshape(-1, 2)
 
 
-def _multi(dist, group=None):
-    return dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1
+def _multi(dist, group=None, always=False):
+    return dist is not None and dist.is_initialized() and (always or dist.get_world_size(group) > 1)
 
 
-def reduce_frame(accum, dist, group=None, async_op=False):
+def reduce_frame(accum, dist, group=None, async_op=False, always=False):
     """Sum every rank's accumulator onto rank 0 (one collective per frame). With async_op the
-    collective's work handle is returned (None without a collective)."""
-    if _multi(dist, group):
+    collective's work handle is returned (None without a collective). always: issue the collective at
+    world size 1 too (an identity there; tests run the RCCL path on a one-GPU box with it)."""
+    if _multi(dist, group, always):
         w = dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
         return w if async_op else accum
     return None if async_op else accum
@@ -54,9 +55,13 @@ class FrameRenderer:
     stream (so accumulators filled there are complete before the first zeroing): a frame's zeroing,
     its render and the collective that reads it must be ordered on one stream the collective waits
     for — a renderer left on its library-owned non-blocking stream would race both.
-    Readers of a frame's accumulator must read on `streams[i]` of that frame or synchronize."""
+    Readers of a frame's accumulator must read on `streams[i]` of that frame or synchronize.
+    `reduce_at_world1` (tests only): issue each frame's reduce even at world size 1, so the pipelined
+    schedule's collective, its async handle and the wait before a buffer's reuse run on RCCL on a
+    one-GPU box."""
 
-    def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None):
+    def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None,
+                 reduce_at_world1=False):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
         self.r, self.dist, self.render_fn = self.rs[0], dist, render_fn
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
@@ -76,6 +81,8 @@ class FrameRenderer:
         self.tile = tile
         self.f = 0
         self.last = None
+        self.reduce_at_world1 = reduce_at_world1
+        self.reduces = 0   # collectives issued
 
     def frame(self, times, first_sample=0):
         """Render this rank's tiles of the next frame and start its reduce; returns the frame's
@@ -94,7 +101,8 @@ class FrameRenderer:
                 else:
                     r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
                     r.render_tiles(times, self.tiles, self.tile, first_sample=first_sample)
-            self.work[i] = reduce_frame(acc, self.dist, async_op=True)
+            self.work[i] = reduce_frame(acc, self.dist, async_op=True, always=self.reduce_at_world1)
+            self.reduces += self.work[i] is not None
         self.f += 1
         self.last = acc
         return acc

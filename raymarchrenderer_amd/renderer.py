@@ -20,9 +20,9 @@ def _fp(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
-def _check(ctx, code):
+def _check(ctx, code, L=None):
     if code != abi.RMR_OK:
-        msg = lib().rmr_last_error(ctx) if ctx else b""
+        msg = (L or lib()).rmr_last_error(ctx) if ctx else b""
         raise RMRError(code, (msg or b"").decode(errors="replace"))
 
 
@@ -67,9 +67,13 @@ def default_camera_view(W, H):
 class Renderer:
     """One rmr context on one GPU (device index `device`)."""
 
-    def __init__(self, device=0, width=1024, height=1024):
+    def __init__(self, device=0, width=1024, height=1024, diag=None):
+        """diag=True: the context lives in the diagnostic build librmr_diag.so, which also reads the
+        experiments' environment switches (RMR_GRID, RMR_JIT_OPTS, ...; tools/, A/B tests); the
+        release librmr.so reads none. None: the release library unless RMR_LIB=diag (tools/)."""
+        self._L = lib(diag=diag)
         self._ctx = C.c_void_p()
-        rc = lib().rmr_create(C.byref(self._ctx), device)
+        rc = self._L.rmr_create(C.byref(self._ctx), device)
         if rc != abi.RMR_OK:
             raise RMRError(rc, "rmr_create failed (no HIP device %d?)" % device)
         self.set_image_size(width, height)
@@ -79,7 +83,7 @@ class Renderer:
     # -- lifetime --
     def close(self):
         if self._ctx:
-            lib().rmr_destroy(self._ctx)
+            self._L.rmr_destroy(self._ctx)
             self._ctx = C.c_void_p()
 
     def __del__(self):
@@ -92,30 +96,38 @@ class Renderer:
     def ctx(self):
         return self._ctx
 
+    @property
+    def lib(self):
+        """The ctypes library this context lives in (librmr.so, or librmr_diag.so with diag=True)."""
+        return self._L
+
+    def _chk(self, code):
+        _check(self._ctx, code, self._L)
+
     # -- configuration --
     def set_image_size(self, w, h):
-        _check(self._ctx, lib().rmr_set_image_size(self._ctx, int(w), int(h)))
+        self._chk(self._L.rmr_set_image_size(self._ctx, int(w), int(h)))
 
     def image_size(self):
         w, h = C.c_int(), C.c_int()
-        _check(self._ctx, lib().rmr_get_image_size(self._ctx, C.byref(w), C.byref(h)))
+        self._chk(self._L.rmr_get_image_size(self._ctx, C.byref(w), C.byref(h)))
         return w.value, h.value
 
     def set_params(self, params=None, **kw):
         p = params if params is not None else abi.default_params()
         for k, v in kw.items():
             setattr(p, k, v)
-        _check(self._ctx, lib().rmr_set_params(self._ctx, C.byref(p)))
+        self._chk(self._L.rmr_set_params(self._ctx, C.byref(p)))
 
     def params(self):
         p = abi.Params()
-        _check(self._ctx, lib().rmr_get_params(self._ctx, C.byref(p)))
+        self._chk(self._L.rmr_get_params(self._ctx, C.byref(p)))
         return p
 
     def set_view(self, view15):
         v = np.ascontiguousarray(view15, np.float32).reshape(15)
         parts = [np.ascontiguousarray(v[3 * i:3 * i + 3]) for i in range(5)]
-        _check(self._ctx, lib().rmr_set_view(self._ctx, *[_fp(x) for x in parts]))
+        self._chk(self._L.rmr_set_view(self._ctx, *[_fp(x) for x in parts]))
         self._view = v
 
     def load_scene(self, scene, variant):
@@ -130,53 +142,58 @@ class Renderer:
         else:
             text = scene
         b = text.encode()
-        _check(self._ctx, lib().rmr_load_scene_json(self._ctx, variant, b, len(b)))
+        self._chk(self._L.rmr_load_scene_json(self._ctx, variant, b, len(b)))
         self.variant = variant
 
     def load_builtin(self, variant):
         if isinstance(variant, str):
             variant = abi.VARIANTS[variant]
-        _check(self._ctx, lib().rmr_load_builtin_scene(self._ctx, variant))
+        self._chk(self._L.rmr_load_builtin_scene(self._ctx, variant))
         self.variant = variant
 
     def load_tables(self, tables):
         s = tables.to_ctypes()
-        _check(self._ctx, lib().rmr_load_scene_tables(self._ctx, C.byref(s)))
+        self._chk(self._L.rmr_load_scene_tables(self._ctx, C.byref(s)))
         self.variant = tables.variant
 
     def reload(self):
-        _check(self._ctx, lib().rmr_reload(self._ctx))
+        self._chk(self._L.rmr_reload(self._ctx))
 
     def set_kernel(self, k):
-        _check(self._ctx, lib().rmr_set_kernel(self._ctx, int(k)))
+        self._chk(self._L.rmr_set_kernel(self._ctx, int(k)))
 
     def set_tuning(self, shade_threshold=0, grid_per_cu=-1, samp_budget=0):
-        _check(self._ctx, lib().rmr_set_tuning(self._ctx, int(shade_threshold), int(grid_per_cu), int(samp_budget)))
+        self._chk(self._L.rmr_set_tuning(self._ctx, int(shade_threshold), int(grid_per_cu), int(samp_budget)))
 
     def set_env_map(self, rgba8):
         """envTex for skyColor (used with params use_env_tex=1): (h, w, 4) uint8, row 0 = up. None clears."""
         if rgba8 is None:
-            _check(self._ctx, lib().rmr_set_env_map(self._ctx, None, 0, 0))
+            self._chk(self._L.rmr_set_env_map(self._ctx, None, 0, 0))
             return
         a = np.ascontiguousarray(rgba8, np.uint8)
         self._env = a
-        _check(self._ctx, lib().rmr_set_env_map(self._ctx, a.ctypes.data, a.shape[1], a.shape[0]))
+        self._chk(self._L.rmr_set_env_map(self._ctx, a.ctypes.data, a.shape[1], a.shape[0]))
 
     def set_jit(self, mode):
         """hipRTC per-scene kernel specialisation: 0 off, 1 always, 2 auto (large launches)."""
-        _check(self._ctx, lib().rmr_set_jit(self._ctx, int(mode)))
+        self._chk(self._L.rmr_set_jit(self._ctx, int(mode)))
+
+    def set_instrument(self, flags):
+        """Instrumented specialised kernels (abi.INSTR_*; rmr_set_instrument): the same images, extra
+        counters (INSTR_COUNT_FLOPS: executed flops per map() in counters() [11..13])."""
+        self._chk(self._L.rmr_set_instrument(self._ctx, int(flags)))
 
     def set_culling(self, flags):
         """Exact work-skipping switches (abi.CULL_*; results are bit-identical either way)."""
-        _check(self._ctx, lib().rmr_set_culling(self._ctx, int(flags)))
+        self._chk(self._L.rmr_set_culling(self._ctx, int(flags)))
 
     def set_stream(self, hip_stream_handle):
-        _check(self._ctx, lib().rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
+        self._chk(self._L.rmr_set_stream(self._ctx, C.c_void_p(hip_stream_handle)))
 
     # -- rendering --
     def render(self, time, vmin, vmax, current_sample):
         """Graphics::Render(currentTime, min, max, currentSample)."""
-        _check(self._ctx, lib().rmr_render(self._ctx, float(time), float(vmin[0]), float(vmin[1]),
+        self._chk(self._L.rmr_render(self._ctx, float(time), float(vmin[0]), float(vmin[1]),
                                            float(vmax[0]), float(vmax[1]), int(current_sample)))
 
     def render_spp(self, times, rect=None, first_sample=0):
@@ -185,49 +202,49 @@ class Renderer:
             w, h = self.image_size()
             rect = (0, 0, w, h)
         x0, y0, x1, y1 = rect
-        _check(self._ctx, lib().rmr_render_spp(self._ctx, _fp(times), x0, y0, x1, y1, int(first_sample), len(times)))
+        self._chk(self._L.rmr_render_spp(self._ctx, _fp(times), x0, y0, x1, y1, int(first_sample), len(times)))
 
     def render_tiles(self, times, tiles_xy, tile_size, first_sample=0):
         times = np.ascontiguousarray(times, np.float32)
         t = np.ascontiguousarray(tiles_xy, np.int32).reshape(-1, 2)
-        _check(self._ctx, lib().rmr_render_tiles(self._ctx, _fp(times), t.ctypes.data_as(C.POINTER(C.c_int32)),
+        self._chk(self._L.rmr_render_tiles(self._ctx, _fp(times), t.ctypes.data_as(C.POINTER(C.c_int32)),
                                                  len(t), int(tile_size), int(first_sample), len(times)))
 
     def trace_samples(self, times, rect):
         times = np.ascontiguousarray(times, np.float32)
         x0, y0, x1, y1 = rect
         out = np.zeros((len(times), y1 - y0, x1 - x0, 4), np.float32)
-        _check(self._ctx, lib().rmr_trace_samples(self._ctx, _fp(times), x0, y0, x1, y1, len(times), _fp(out)))
+        self._chk(self._L.rmr_trace_samples(self._ctx, _fp(times), x0, y0, x1, y1, len(times), _fp(out)))
         return out
 
     def sync(self):
-        _check(self._ctx, lib().rmr_sync(self._ctx))
+        self._chk(self._L.rmr_sync(self._ctx))
 
     def read_accum(self):
         w, h = self.image_size()
         out = np.zeros((h, w, 4), np.float32)
-        _check(self._ctx, lib().rmr_read_accum(self._ctx, _fp(out), out.nbytes))
+        self._chk(self._L.rmr_read_accum(self._ctx, _fp(out), out.nbytes))
         return out
 
     def write_accum(self, a):
         a = np.ascontiguousarray(a, np.float32)
-        _check(self._ctx, lib().rmr_write_accum(self._ctx, _fp(a), a.nbytes))
+        self._chk(self._L.rmr_write_accum(self._ctx, _fp(a), a.nbytes))
 
     def accum_device_ptr(self):
-        return lib().rmr_accum_device_ptr(self._ctx)
+        return self._L.rmr_accum_device_ptr(self._ctx)
 
     def bind_accum(self, dev_ptr, nbytes):
-        _check(self._ctx, lib().rmr_bind_accum(self._ctx, C.c_void_p(dev_ptr), int(nbytes)))
+        self._chk(self._L.rmr_bind_accum(self._ctx, C.c_void_p(dev_ptr), int(nbytes)))
 
     def save_bmp(self, path):
-        _check(self._ctx, lib().rmr_save_bmp(self._ctx, path.encode()))
+        self._chk(self._L.rmr_save_bmp(self._ctx, path.encode()))
 
     def save_accum(self, path, samples_done):
-        _check(self._ctx, lib().rmr_save_accum(self._ctx, path.encode(), int(samples_done)))
+        self._chk(self._L.rmr_save_accum(self._ctx, path.encode(), int(samples_done)))
 
     def load_accum(self, path):
         n = C.c_uint32()
-        _check(self._ctx, lib().rmr_load_accum(self._ctx, path.encode(), C.byref(n)))
+        self._chk(self._L.rmr_load_accum(self._ctx, path.encode(), C.byref(n)))
         return n.value
 
     def display(self, centre, zoom, vmin, vmax, screen=None, screen_size=None):
@@ -241,38 +258,50 @@ class Renderer:
         if screen.ndim != 3 or screen.shape[2] != 4:
             raise ValueError("display: screen must be an (h, w, 4) RGBA8 image, got shape %s" % (screen.shape,))
         h, w = screen.shape[:2]
-        _check(self._ctx, lib().rmr_display(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
+        self._chk(self._L.rmr_display(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
                                             float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
                                             w, h, screen.ctypes.data, screen.nbytes))
         return screen
 
-    def display_device(self, centre, zoom, vmin, vmax, dev_ptr, screen_w, screen_h, nbytes=None):
-        """rmr_display_device: the same into a device RGBA8 buffer of `nbytes` bytes (default
-        screen_w * screen_h * 4) on the renderer's stream."""
-        if nbytes is None:
-            nbytes = int(screen_w) * int(screen_h) * 4
-        _check(self._ctx, lib().rmr_display_device(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
+    def display_device(self, centre, zoom, vmin, vmax, dev, screen_w, screen_h, nbytes=None):
+        """rmr_display_device: the same into a device RGBA8 buffer on the renderer's stream. `dev` is a
+        torch tensor on the GPU (its size is numel * element_size) or a raw device pointer, which needs
+        `nbytes`, the buffer's size in bytes (the library checks it against screen_w * screen_h * 4)."""
+        if hasattr(dev, "data_ptr"):
+            if not dev.is_contiguous():
+                raise ValueError("display_device: the tensor must be contiguous")
+            size = dev.numel() * dev.element_size()
+            if nbytes is not None and int(nbytes) > size:
+                raise ValueError("display_device: nbytes %d exceeds the tensor's %d bytes" % (nbytes, size))
+            nbytes = size if nbytes is None else int(nbytes)
+            dev_ptr = dev.data_ptr()
+        else:
+            if nbytes is None:
+                raise ValueError("display_device: a raw device pointer needs nbytes (the buffer's size in bytes)")
+            dev_ptr = int(dev)
+        self._chk(self._L.rmr_display_device(self._ctx, float(centre[0]), float(centre[1]), float(zoom),
                                                    float(vmin[0]), float(vmin[1]), float(vmax[0]), float(vmax[1]),
                                                    int(screen_w), int(screen_h), C.c_void_p(dev_ptr), int(nbytes)))
 
     def stats(self):
         s = abi.Stats()
-        _check(self._ctx, lib().rmr_get_stats(self._ctx, C.byref(s)))
+        self._chk(self._L.rmr_get_stats(self._ctx, C.byref(s)))
         return s
 
     def reset_stats(self):
-        _check(self._ctx, lib().rmr_reset_stats(self._ctx))
+        self._chk(self._L.rmr_reset_stats(self._ctx))
 
     def counters(self):
         """The kernels' 16 raw device counters (rmr_get_counters; rmr_trace.h documents the slots)."""
         raw = (C.c_uint64 * 16)()
-        _check(self._ctx, lib().rmr_get_counters(self._ctx, raw))
+        self._chk(self._L.rmr_get_counters(self._ctx, raw))
         return [int(v) for v in raw]
 
 
-def jit_compile_scene(scene, variant):
+def jit_compile_scene(scene, variant, diag=None):
     """Compile the hipRTC-specialised trace kernel of a scene (no GPU needed). Returns the
-    code-object key; raises RMRError with the compiler log on failure."""
+    code-object key; raises RMRError with the compiler log on failure. diag: through the
+    diagnostic build (which reads the experiments' RMR_JIT_* environment switches)."""
     if isinstance(variant, str):
         variant = abi.VARIANTS[variant]
     if scene is None:
@@ -284,7 +313,7 @@ def jit_compile_scene(scene, variant):
     else:
         text = scene.encode()
     log = C.create_string_buffer(65536)
-    rc = lib().rmr_jit_compile_scene(int(variant), text or None, len(text), log, len(log))
+    rc = lib(diag=diag).rmr_jit_compile_scene(int(variant), text or None, len(text), log, len(log))
     if rc != abi.RMR_OK:
         raise RMRError(rc, log.value.decode(errors="replace"))
     return log.value.decode()

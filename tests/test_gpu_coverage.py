@@ -182,6 +182,42 @@ def test_full_c4_frame_properties_and_sampled_tiles(renderer):
     assert st.map_evals > 0
 
 
+@pytest.mark.timeout(300)
+def test_c4_production_launch_sampled_pixels_bitexact(renderer):
+    """C4 exactly as the bench renders it: 3840x2160 at 256 spp, 4 bounces, all 32x32 tiles in ONE
+    launch (2.12e9 units, unit indices up to 2^31 - 2^25; 34 GB of sample planes, so plane offsets far
+    beyond 4 GiB; rmr_trace.h unit_pixel / fold_main). Three pixels — the frame's last one (the highest
+    tile and plane offsets), the brightest and a median one — are checked bitwise against the oracle's
+    running mean of all 256 samples (RM1:600-612 folds every sample in order, so each pixel is a check
+    of its 256 per-sample radiances through the fold)."""
+    from raymarchrenderer_amd.multi_gpu import frame_tiles
+    W, H, spp = 3840, 2160, 256
+    path = os.path.join(SCENES, "csg256.scene")
+    prm, view = _setup(renderer, path, W, H, max_bounces=4)
+    times = time_schedule(spp)
+    renderer.set_jit(1)
+    try:
+        renderer.reset_stats()
+        renderer.render_tiles(times, frame_tiles(W, H, 32), 32)
+        img = renderer.read_accum()
+        st = renderer.stats()
+    finally:
+        renderer.set_jit(2)
+        renderer.set_image_size(64, 64)   # release the 34 GB of planes' frame
+        renderer.reload()
+    assert st.jit_launches == st.trace_launches == 1
+    assert st.samples == W * H * spp
+    assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and (img[..., 3] == 1.0).all()
+    lum = img[..., :3].sum(-1)
+    flat = np.argsort(lum.ravel())
+    picks = [(W - 1, H - 1), (int(flat[-1] % W), int(flat[-1] // W)), (int(flat[flat.size // 2] % W), int(flat[flat.size // 2] // W))]
+    orc = oracle.Oracle(scene_compile.load_scene_file(path, "rm1"), prm, view, W, H)
+    for x, y in picks:
+        cpu = orc.render(times, rect=(x, y, x + 1, y + 1))
+        eq = _same(img[y, x], cpu[y, x])
+        assert eq.all(), "pixel (%d, %d): gpu %s oracle %s" % (x, y, img[y, x], cpu[y, x])
+
+
 def test_full_c5_frame_properties_and_sampled_tiles(renderer):
     """C5 (BASELINE configs[4]): an animated frame (f = 37, the sphere moved: the live-primitive
     kernel) at 1920x1080, 4 bounces, on the bench's large-seed schedule; 2 spp instead of 512.

@@ -2,13 +2,16 @@
 
 RCCL refuses two ranks on one device, so the N > 1 schedule is rehearsed on one GPU over gloo
 (test_gpu_multi_rank.py) and the RCCL collective itself only runs in the driver's 8-GPU run. This
-test runs RCCL here at world size 1 (backend "nccl" = RCCL on ROCm): a process group initialised the
-way bench.py initialises it (`device_id` = the rank's GPU), a frame rendered by FrameRenderer on its
-torch stream into a device accumulator, then the two collectives bench.py's N > 1 path issues on
-device tensors — `dist.reduce(SUM, dst=0)` of the accumulator (multi_gpu.reduce_frame, ordered on the
-frame's stream, async work handle waited) and `dist.all_gather` of the per-rank timing row. At world
-size 1 the reduce is an identity, so the accumulator must come back bit for bit the one-context render
-of the whole frame. The script runs in a child process so its process group never meets pytest's."""
+test runs RCCL here at world size 1 (backend "nccl" = RCCL on ROCm), through the product's own
+pipelined schedule: a process group initialised the way bench.py initialises it (`device_id` = the
+rank's GPU), then FrameRenderer with `reduce_at_world1` (its test-only switch: issue the collective
+although the world has one rank) rendering three frames into two device accumulators on two renderer
+contexts and streams. Each frame() zeroes its buffer, renders, and issues multi_gpu.reduce_frame's
+`dist.reduce(SUM, dst=0, async_op=True)` on the frame's stream; frame 3 reuses frame 1's buffer, so it
+first waits on that reduce's work handle; finish() waits for the rest. At world size 1 the reduce is
+an identity, so every frame's accumulator must come back bit for bit the one-context render of the
+whole frame. bench.py's `dist.all_gather` of the per-rank timing row runs too. The script runs in a
+child process so its process group never meets pytest's."""
 import os
 import socket
 import subprocess
@@ -41,33 +44,41 @@ def mk():
     r.set_view(camera.default_view(W, H))
     return r
 
-times = time_schedule(SPP)
-r = mk()
+frames = [time_schedule(SPP, frame=f) for f in range(3)]
+rs = [mk(), mk()]
 accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
-fr = FrameRenderer([r], accs, W, H, TILE, 0, 1, dist)
-fr.frame(times)
-acc = fr.finish()
-s = fr.streams[0]
-with torch.cuda.stream(s):
-    work = dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM, async_op=True)
-    work.wait()
+fr = FrameRenderer(rs, accs, W, H, TILE, 0, 1, dist, reduce_at_world1=True)
+snaps = []
+for f in range(3):
+    acc = fr.frame(frames[f])   # frame f + 1 renders while frame f's reduce is in flight
+    i = f % 2
+    with torch.cuda.stream(fr.streams[i]):
+        fr.work[i].wait()           # stream-ordered (no host block): the copy runs after the reduce,
+        snaps.append(acc.clone())   # and before frame f + 2 zeroes the buffer on the same stream
+fr.finish()
+torch.cuda.synchronize()
+got = [x.cpu().numpy() for x in snaps]
+assert fr.reduces == 3, fr.reduces
+with torch.cuda.stream(fr.streams[0]):
     row = torch.tensor([1.0, 2.0, 3.0], dtype=torch.float64, device="cuda")
     rows = [torch.zeros_like(row)]
     dist.all_gather(rows, row)
-s.synchronize()
-got = acc.cpu().numpy()
+fr.streams[0].synchronize()
 assert rows[0].cpu().tolist() == [1.0, 2.0, 3.0]
-r.close()
+for r in rs:
+    r.close()
 
-r1 = mk()
-r1.render_tiles(times, frame_tiles(W, H, TILE), TILE)
-want = r1.read_accum()
-r1.close()
+ndiff = 0
+for f in range(3):
+    r1 = mk()
+    r1.render_tiles(frames[f], frame_tiles(W, H, TILE), TILE)
+    want = r1.read_accum()
+    r1.close()
+    assert np.isfinite(want).all() and (want[..., 3] == 1.0).all()
+    ndiff += int((got[f].view(np.uint32) != want.view(np.uint32)).sum())
 dist.destroy_process_group()
-diff = got.view(np.uint32) != want.view(np.uint32)
-assert np.isfinite(want).all() and (want[..., 3] == 1.0).all()
-print("rccl ok: reduce + all_gather at world 1, %d differing words" % int(diff.sum()))
-sys.exit(1 if diff.any() else 0)
+print("rccl ok: 3 pipelined frames reduced at world 1 + all_gather, %d differing words" % ndiff)
+sys.exit(1 if ndiff else 0)
 """
 
 

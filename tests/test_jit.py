@@ -44,15 +44,41 @@ def test_jit_source_compiles_for_gfx950(tmp_path, monkeypatch, name, path, varia
 
 def test_jit_scheduler_directive(tmp_path, monkeypatch):
     """The inline approximate-map kernels (Cornell-5) carry an `//@opts` scheduler directive
-    (rmr_jit.cpp): it reaches hipRTC (another code object under another key); RMR_JIT_SCHED=0 drops it."""
+    (rmr_jit.cpp): it reaches hipRTC (another code object under another key); RMR_JIT_SCHED=0 drops it
+    in the diagnostic build."""
     path = os.path.join(SCENES, "cornell5.scene")
     monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path))
-    k_on = jit_compile_scene(path, "rm1")
+    k_on = jit_compile_scene(path, "rm1", diag=True)
     monkeypatch.setenv("RMR_JIT_SCHED", "0")
-    k_off = jit_compile_scene(path, "rm1")
+    k_off = jit_compile_scene(path, "rm1", diag=True)
     assert k_on != k_off
     on, off = (tmp_path / (k_on + ".hsaco")).read_bytes(), (tmp_path / (k_off + ".hsaco")).read_bytes()
     assert on != off
+
+
+def test_release_library_ignores_environment(tmp_path, monkeypatch):
+    """The release librmr.so reads no environment switch but RMR_JIT_CACHE: with the experiments'
+    switches set (every one the diagnostic build reads), it compiles the same code object as without
+    them, and their names are not in the binary; librmr_diag.so does read them."""
+    from raymarchrenderer_amd._lib import LIB_DIAG_PATH, LIB_PATH
+    path = os.path.join(SCENES, "cornell5.scene")
+    monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path))
+    k0 = jit_compile_scene(path, "rm1", diag=False)
+    switches = {"RMR_JIT_SCHED": "0", "RMR_JIT_OPTS": "-DRMR_PROG_WAVES=7", "RMR_JIT_BAKE": "0", "RMR_JIT_CULL": "3",
+                "RMR_JIT_STEP": "0", "RMR_JIT_BKEY": "0", "RMR_JIT_AMBCOUNT": "1", "RMR_ESC_BOXES": "4",
+                "RMR_GRID": "0", "RMR_JIT": "0", "RMR_ESC": "0", "RMR_NPC": "0", "RMR_JIT_APPROX": "0", "RMR_EYE": "0"}
+    for k, v in switches.items():
+        monkeypatch.setenv(k, v)
+    assert jit_compile_scene(path, "rm1", diag=False) == k0
+    assert jit_compile_scene(path, "rm1", diag=True) != k0
+    import re
+    rel = set(m.decode() for m in re.findall(rb"(RMR_[A-Z0-9_]+)\x00", open(LIB_PATH, "rb").read()))
+    dia = set(m.decode() for m in re.findall(rb"(RMR_[A-Z0-9_]+)\x00", open(LIB_DIAG_PATH, "rb").read()))
+    env_names = set(switches) | {"RMR_SHADE_T", "RMR_REFILL_T", "RMR_FULL_T", "RMR_FULL_R", "RMR_NPC_KSEL",
+                                 "RMR_BVH_LEAF", "RMR_GRID_CELLS", "RMR_GRID_PAD", "RMR_GRID_PER_CU", "RMR_JIT_DUMP"}
+    assert not (rel & env_names), sorted(rel & env_names)
+    assert env_names <= dia, sorted(env_names - dia)
+    assert "RMR_JIT_CACHE" in rel
 
 
 def _setup(r, path, variant, W, H, overrides):
@@ -355,6 +381,39 @@ def test_culling_switches_bitexact(renderer, scene, bounces, spp):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("step_mult", [1.5, 2.0])
+def test_escape_bound_inside_rays_long_steps_bitexact(renderer, step_mult):
+    """Inside marches (glass, distMult = -1, RM1:498-505) take no escape bound: a step longer than the
+    distance to the surface (stepMultiply > 1, rmr_params.step_multiply) can carry an inside ray past
+    its object's box in one step, where the reference's next map() is positive and -map < 0.001 is a
+    hit, not a miss. Every switch on and off, JIT and table kernels, and the oracle agree bitwise."""
+    W, H = 96, 64
+    path = os.path.join(GOLDEN, "scenes", "glass_test.scene")
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 8, "step_multiply": step_mult})
+    times = time_schedule(4, frame=2)
+    out = {}
+    try:
+        for jit in (1, 0):
+            renderer.set_jit(jit)
+            for flags in (abi.CULL_ALL, 0):
+                renderer.set_culling(flags)
+                renderer.reload()
+                out[(jit, flags)] = renderer.trace_samples(times, (0, 0, W, H))
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+        renderer.set_jit(2)
+    ref = out[(0, 0)]
+    for k, img in out.items():
+        same = (img.view(np.uint32) == ref.view(np.uint32)).all(-1) | (np.isnan(img).any(-1) & np.isnan(ref).any(-1))
+        assert same.all(), "%s: %d samples differ" % (k, (~same).sum())
+    rect = (20, 10, 60, 40)
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = out[(1, abi.CULL_ALL)][:, rect[1]:rect[3], rect[0]:rect[2], :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ from the oracle" % (~same.all(-1)).sum()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene,W,H", [("cornell5.scene", 1920, 1080), ("csg256.scene", 960, 540),
                                        ("rm2:simple.scene", 1920, 1080), ("default.scene", 960, 540)])
 def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
@@ -382,21 +441,23 @@ def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene", ["csg256.scene", "csg64.scene"])
-def test_candidate_grid_full_frame_bitexact(renderer, monkeypatch, scene):
+def test_candidate_grid_full_frame_bitexact(monkeypatch, scene):
     """The nearest-primitive cache's full map() through the candidate grid (rmr_trace.h map_grid_npc,
     the default for BVH scenes) against the same cache over the BVH traversal (RMR_GRID=0, read at
-    scene load): every sample of a 960x540 2-spp frame bitwise equal."""
+    scene load by the diagnostic build): every sample of a 960x540 2-spp frame bitwise equal."""
+    from raymarchrenderer_amd import Renderer
     W, H = 960, 540
     out = {}
-    renderer.set_jit(1)
+    r = Renderer(0, 64, 64, diag=True)
+    r.set_jit(1)
     try:
         for grid in ("1", "0"):
             monkeypatch.setenv("RMR_GRID", grid)
-            _setup(renderer, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
-            out[grid] = renderer.trace_samples(time_schedule(2, frame=9), (0, 0, W, H))
+            _setup(r, os.path.join(SCENES, scene), "rm1", W, H, {"max_bounces": 4})
+            out[grid] = r.trace_samples(time_schedule(2, frame=9), (0, 0, W, H))
     finally:
         monkeypatch.delenv("RMR_GRID")
-        renderer.set_jit(2)
+        r.close()
     a, b = out["1"], out["0"]
     same = (a.view(np.uint32) == b.view(np.uint32)).all(-1) | (np.isnan(a).any(-1) & np.isnan(b).any(-1))
     assert same.all(), "%d of %d samples differ" % ((~same).sum(), same.size)
@@ -506,18 +567,20 @@ def test_jit_rm2_v2_program_bitexact_vs_oracle(renderer, tmp_path, prog):
 
 def test_jit_stepped_mandelbulb_source(tmp_path, monkeypatch):
     """Scenes with one Mandelbulb get the stepped map (rmr_trace.h MBStep: begin / step / finish,
-    finishing batches); RMR_JIT_STEP=0 keeps the whole map per pass (another code object)."""
+    finishing batches); RMR_JIT_STEP=0 keeps the whole map per pass (another code object; the
+    diagnostic build, which also dumps the source with RMR_JIT_DUMP)."""
     path = os.path.join(SCENES, "mandelbulb.scene")
     monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path / "c"))
     (tmp_path / "d").mkdir()
     monkeypatch.setenv("RMR_JIT_DUMP", str(tmp_path / "d"))
-    k_on = jit_compile_scene(path, "rm1")
+    k_on = jit_compile_scene(path, "rm1", diag=True)
+    assert jit_compile_scene(path, "rm1", diag=False) == k_on   # the release build's kernel
     src = (tmp_path / "d" / (k_on + ".hip")).read_text()
     assert "kStepped = RMR_MB_STEPPED" in src and "mb_step(s, " in src and "mb_de(s.r, s.dr)" in src
     monkeypatch.setenv("RMR_JIT_STEP", "0")
-    k_off = jit_compile_scene(path, "rm1")
+    k_off = jit_compile_scene(path, "rm1", diag=True)
     assert k_off != k_on
     assert "kStepped = false" in (tmp_path / "d" / (k_off + ".hip")).read_text()
     # a sphere/box scene has no stepped map
-    k_c5 = jit_compile_scene(os.path.join(SCENES, "cornell5.scene"), "rm1")
+    k_c5 = jit_compile_scene(os.path.join(SCENES, "cornell5.scene"), "rm1", diag=True)
     assert "kStepped = false" in (tmp_path / "d" / (k_c5 + ".hip")).read_text()

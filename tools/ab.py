@@ -13,6 +13,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 import numpy as np  # noqa: E402
 from raymarchrenderer_amd import abi, time_schedule  # noqa: E402
 
@@ -72,6 +73,7 @@ def main():
     times = time_schedule(args.spp)
     tp = times.ctypes.data_as(C.POINTER(C.c_float))
     res = {p: [] for p, _, _ in ctxs}
+    stats = {}
     imgs = {}
     for rnd in range(args.rounds + 1):
         for p, L, h in ctxs:
@@ -81,6 +83,7 @@ def main():
             L.rmr_get_stats(h, C.byref(st))
             if rnd > 0:
                 res[p].append(st.trace_ms)
+            stats[p] = st
             if rnd == args.rounds and hasattr(L, "rmr_get_section_cycles"):
                 cy = (C.c_uint64 * 4)()
                 L.rmr_get_section_cycles(h, cy)
@@ -97,9 +100,12 @@ def main():
     for p in args.libs:
         t = np.array(res[p])
         same = np.array_equal(imgs[p].view(np.uint32), imgs[base].view(np.uint32))
+        st = stats[p]
         print(json.dumps({"lib": os.path.basename(p), "median_ms": round(float(np.median(t)), 3),
                           "min_ms": round(float(t.min()), 3),
                           "Msamples/s": round(args.W * args.H * args.spp / np.median(t) / 1e3, 1),
+                          "map_evals": int(st.map_evals), "map_iters": int(st.map_iters),
+                          "shade_batches": int(st.shade_batches),
                           "bitwise_equal_to_first": bool(same)}), flush=True)
 
 

@@ -3,6 +3,7 @@
 # working tree's librmr.so on every hot kernel class: Cornell-5 (C2), RM3 builtin, the Mandelbulb (C3),
 # csg256 (C4) and RM2 simple.scene, 1080p; bitwise comparison of the accumulators included.
 #   SPP (default 16), ROUNDS (default 6), CASES (default: all five)
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 S=${SPP:-16}; R=${ROUNDS:-6}

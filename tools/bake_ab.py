@@ -5,6 +5,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 import numpy as np  # noqa: E402
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
 

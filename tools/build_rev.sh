@@ -13,6 +13,7 @@ if [ "$REV" = WT ]; then
 else
   git -C "$ROOT" archive "$REV" raymarchrenderer_amd/csrc include | tar -x -C "$T"
 fi
-make -s -C "$T/raymarchrenderer_amd/csrc" -j8 BUILD="$T/build" OUT="$OUT" EXTRA="$EXTRA"
+TGT=$(grep -q "^lib:" "$T/raymarchrenderer_amd/csrc/Makefile" && echo lib || true)   # (older revisions: no lib target)
+make -s -C "$T/raymarchrenderer_amd/csrc" -j8 $TGT BUILD="$T/build" OUT="$OUT" EXTRA="$EXTRA"
 rm -rf "$T"
 echo "built $OUT from $REV"

@@ -2,6 +2,7 @@
 # C3 (Mandelbulb): the stepped map (finishing batches of RMR_MB_FIN lanes) against the whole map per
 # pass (-DRMR_MB_STEPPED=0), finishing-batch sizes and waves per SIMD, same process; then the
 # Mandelbulb GPU parity tests
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 A="--scenes mandelbulb --spp ${SPP:-32} --rounds ${ROUNDS:-5}"

@@ -1,5 +1,6 @@
 #!/bin/bash
 # csg256 (C4's scene) sweeps of load-time knobs: grid cell count and region pad
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 timeout -k 10 400 python tools/env_ab.py RMR_GRID_CELLS 1048576 2097152 4194304 8388608 --scenes csg256 --spp 8 --rounds 3 > gpurun_out/c4_cells.log 2>&1 || exit $?

@@ -1,3 +1,4 @@
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd /root/repo
 for o in -O3 -DRMR_CHUNK=64 -DRMR_CHUNK=32; do
   for spp in 4 16 64; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # The escape bound for every kernel class (round 3: RM2 incl. shadow rays, node-program-material
 # kernels): tools/librmr_base.so (HO kernels only) against the working tree, same process, bitwise.
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 : > gpurun_out/esc_ab.log

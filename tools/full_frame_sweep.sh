@@ -1,6 +1,7 @@
 #!/bin/bash
 # Full-frame bitwise sweep of the exact work-skipping paths (rmr_set_culling all on vs all off) per
 # scene family, at production sizes; differing samples are checked against the CPU oracle.
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 O=gpurun_out/full_frame_sweep.log; : > $O

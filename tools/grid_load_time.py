@@ -1,6 +1,7 @@
 """Scene-load time of csg256 per candidate-grid size (RMR_GRID_CELLS), and without the grid."""
 import os, sys, time
 sys.path.insert(0, os.getcwd())
+os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 from raymarchrenderer_amd import Renderer
 r = Renderer(0, 256, 256)
 for cells in ("65536", "131072", "262144", "524288", "1048576"):

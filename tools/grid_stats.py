@@ -12,6 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 os.environ["RMR_JIT_OPTS"] = (os.environ.get("RMR_JIT_OPTS", "") + " -DRMR_GRID_STATS").strip()
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
 from raymarchrenderer_amd._lib import lib  # noqa: E402

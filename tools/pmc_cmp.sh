@@ -2,6 +2,7 @@
 # PMC instruction counts + kernel counters of one render per setting (tools/stats_run.py under rocprofv3
 # --pmc; separate runs per setting). Usage: tools/pmc_cmp.sh TAG "ENV=.. ARGS" ["ENV=.. ARGS" ...]
 #   e.g. tools/pmc_cmp.sh grid "RMR_GRID=1" "RMR_GRID=0"
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 TAG=$1; shift

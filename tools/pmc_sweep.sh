@@ -1,6 +1,7 @@
 #!/bin/bash
 # VALU/SALU instruction counts of the trace kernel per tuning setting (shade / refill thresholds):
 # the slopes against the counters of tools/stats_run.py give the per-batch instruction costs.
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sweep

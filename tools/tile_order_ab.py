@@ -1,5 +1,6 @@
 import os, sys, json
 sys.path.insert(0, "/root/repo")
+os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 import numpy as np
 from raymarchrenderer_amd import Renderer, abi, time_schedule
 from raymarchrenderer_amd.multi_gpu import tile_partition

@@ -1,6 +1,7 @@
 #!/bin/bash
 # HBM traffic (FETCH_SIZE / WRITE_SIZE, separate rocprofv3 passes) of one tools/stats_run.py render per
 # setting. Usage: tools/traffic_cmp.sh TAG "ENV=.. ARGS" ["ENV=.. ARGS" ...]
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 TAG=$1; shift

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Occupancy / scheduler sweeps of the specialised kernels (RMR_JIT_OPTS / RMR_JIT_SCHED are part of the
 # code-object key, so one process compiles each variant): csg256 (cache kernels), Mandelbulb, RM3
+export RMR_LIB=diag   # tools run against the diagnostic build (env switches)
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 timeout -k 10 400 python tools/env_ab.py RMR_JIT_OPTS --scenes csg256 --spp 8 --rounds 3 -- " " "-DRMR_CACHE_WAVES=5" "-DRMR_CACHE_WAVES=7" > gpurun_out/w_c4.log 2>&1 || exit $?
