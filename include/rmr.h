@@ -159,7 +159,7 @@ int rmr_reset_stats(rmr_ctx* ctx);
 int rmr_get_section_cycles(rmr_ctx* ctx, uint64_t out[4]);
 /* Raw kernel counters (diagnostics): [0] map evals, [1] map iterations, [2] shading batches,
  * [3] full map() batches of the nearest-primitive cache, [8] lanes shaded (lane-level shading events),
- * [14] map evals in shading batches (certified getNormal probes, rmr_trace.h normal_from_prim; part of [0]),
+ * [14] map evals in shading batches (certified getNormal probes, rmr_trace.h cert_normals; part of [0]),
  * [4..7] the section cycles above (or the RMR_JIT_AMBCOUNT fallback counts, tools/amb_rate.py). */
 int rmr_get_counters(rmr_ctx* ctx, uint64_t out[16]);
 /* Select kernel implementation (0 = persistent wavefront kernel, 1 = one launch-thread per path). */

@@ -725,6 +725,12 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
             E = std::max(E, std::max({std::fabs(q.c[0]), std::fabs(q.c[1]), std::fabs(q.c[2])}) + rr);
         }
         P.npc_eps0 = E * 0x1p-17f + 0x1p-60f;
+        // rmr_trace.h am_normal_cert: (0.002 + 2R) 2^-20 + 2^-39 + 4 eps + 2 delta with eps the npc_eps
+        // bound at |p|_inf <= E + 0.005 (a hit's probes), in double, widened by 2^-20 for the kernel
+        // fma's rounding and rounded up to float
+        const double eps = ((double)E + 0.005) * 0x1p-17 + (double)P.npc_eps0;
+        const double k0 = (0.002 + (double)P.am_r2) * 0x1p-20 + 0x1p-39 + 4.0 * eps + 2.0 * 0.0010001;
+        P.cert_k = std::nextafter((float)(k0 * (1.0 + 0x1p-20)), INFINITY);
     }
     P.full_threshold = c->full_threshold;
     {
@@ -778,6 +784,13 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         P.r10[i] = c->view[9 + i]; P.r11[i] = c->view[12 + i];
     }
     P.W = c->W; P.H = c->H;
+    for (int i = 0; i < 3; i++) {
+        P.dr01[i] = P.r01[i] - P.r00[i];   // float subtraction: the bits fmix's y - x gives
+        P.dr11[i] = P.r11[i] - P.r10[i];
+    }
+    P.Wf = (float)c->W; P.Hf = (float)c->H;
+    P.env_wf[0] = (float)c->env_w; P.env_wf[1] = (float)c->env_h;
+    P.env_wf[2] = (float)(c->env_w - 1); P.env_wf[3] = (float)(c->env_h - 1);
     P.x0 = x0; P.y0 = y0; P.x1 = x1; P.y1 = y1;
     P.tiles = c->d_tiles;
     P.n_tiles = (int)tiles.size();

@@ -75,6 +75,7 @@ struct KParams {
     float bvh_margin;           // absolute part of the culling margin (scales with the scene extent)
     float am_r2;                // 2 x the largest |sphere radius| (approximate-then-exact map, rmr_trace.h)
     float npc_eps0;             // nearest-primitive cache: 2^-17 E + 2^-60 (rmr_trace.h npc_eps)
+    float cert_k;               // certified getNormal probes: the bound of rmr_trace.h am_normal_cert
     int32_t esc_on;             // escape bound (rmr_trace.h ray_exit): sphere/box scenes
     int32_t eye_step;           // primary rays' first march step from map(eye) (rmr_trace.h eye_map)
     const float* esc_boxes;     // n_esc inflated boxes (lo.xyz, hi.xyz) covering every primitive
@@ -97,6 +98,12 @@ struct KParams {
     // ---- view (setView uniforms, shader order) ----
     float eye[3], r00[3], r01[3], r10[3], r11[3];
     int32_t W, H;
+    // host-computed uniforms the kernels would otherwise derive per wave with VALU ops (whose results
+    // the allocator keeps in VGPRs for the whole kernel, and spills): r01 - r00, r11 - r10 (float
+    // subtraction, the same bits), (float)W, (float)H, and the env map's (float) w, h, w - 1, h - 1
+    float dr01[3], dr11[3];
+    float Wf, Hf;
+    float env_wf[4];
     // ---- work ----
     int32_t x0, y0, x1, y1;     // clip rect (pixels inside = rendered)
     const TileXY* tiles;        // n_tiles tiles

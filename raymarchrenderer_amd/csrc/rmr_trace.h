@@ -575,20 +575,20 @@ RMR_D V2 am_result_packed(const KParams& P, const AMin& m) {
     return d;
 }
 #define NPC_PROBE_DELTA 0.0010001f
-// Certificate, at a march point p, that getNormal's six probes p +- h e_c (RM1:259-268) all have w as
-// the unique minimiser of the opU fold, so each probe's map() is opU((maxDist, -1), F_w(probe), id_w)
-// (the fold's closed form, map_bvh) and its distance is primitive w's alone. With eps = npc_eps over
-// the probes' box (float evaluation error of any box/sphere distance, 4x slack; npc_eps below) and
-// delta = NPC_PROBE_DELTA >= |probe - p|, SDFs being 1-Lipschitz:
+// Certificate, at a hit, that getNormal's six probes p +- h e_c (RM1:259-268) all have w as the unique
+// minimiser of the opU fold, so each probe's map() is opU((maxDist, -1), F_w(probe), id_w) (the fold's
+// closed form, map_bvh) and its distance is primitive w's alone. With eps the float evaluation error of
+// any box/sphere distance at the probes (npc_eps, 4x slack) and delta = NPC_PROBE_DELTA >= |probe - p|,
+// SDFs being 1-Lipschitz:
 //   F_w(probe) <= a + err(a) + 2 eps + delta,   F_j(probe) >= s2 - err(s2) - 2 eps - delta  (j != w),
 // a / s2 the approximate minimum / runner-up (am_*: |a_j - F_j| <= err(a_j) = 2^-21 (|a_j| + R) +
-// 2^-40, monotonic in a_j). So s2 - a > err(a) + err(s2) + 4 eps + 2 delta suffices; the test below
-// takes am_unique's doubled margin and |s2| + |a| 2^-20 for its own rounding. NaN: false.
-RMR_D bool am_normal_cert(const KParams& P, const AMin& m, V3 p, float R2) {
-    const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
-    const float eps = fmaf(ax + 0.002f, 0x1p-17f, P.npc_eps0);
-    const float margin = fmaf(fabsf(m.a) + fabsf(m.s2) + R2, 0x1p-20f, 0x1p-39f);
-    return m.s2 - m.a > fmaf(4.0f, eps, margin + 2.0f * NPC_PROBE_DELTA);
+// 2^-40, monotonic in a_j). So s2 - a > err(a) + err(s2) + 4 eps + 2 delta suffices. At a hit the
+// point is within ~0.002 of primitive w, so |p|_inf <= E + 0.003 (E = max |c|_inf + |r|_inf) and eps
+// is a per-scene constant; with |a| < 0.002 the test becomes s2 (1 - 2^-20) - a > K (host, rmr_api.cpp
+// cert_k: (0.002 + 2R) 2^-20 + 2^-39 + 4 eps(E + 0.005) + 2 delta, widened for this fma's rounding,
+// with am_unique's doubled error terms). NaN: false. Meaningful at hits only (march_update uses it so).
+RMR_D bool am_normal_cert(const KParams& P, const AMin& m) {
+    return (fabsf(m.a) < 0.002f) & (fmaf(m.s2, 1.0f - 0x1p-20f, -m.a) > P.cert_k);
 }
 
 // One scalar load per prim (the 32-byte DPrim as a single s_load_dwordx8), with prim j+1's load
@@ -1166,12 +1166,14 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
     if (phi < 0.0f) phi += 2.0f * PI;
     const float s = phi / (2.0f * PI);
     const float t = 1.0f - (dir.y * 0.5f + 0.5f);
-    const int W = P.env_w, H = P.env_h;
-    const float fu = s * (float)W - 0.5f, fv = t * (float)H - 0.5f;
+    const int W = P.env_w;
+    // (float)W, (float)H, (float)(W - 1), (float)(H - 1) come converted from the host (kernel
+    // arguments, scalar operands) instead of VALU conversions the allocator keeps live and spills
+    const float fu = s * P.env_wf[0] - 0.5f, fv = t * P.env_wf[1] - 0.5f;
     const float i0f = floorf(fu), j0f = floorf(fv);
     const float a = fu - i0f, b = fv - j0f;
-    const int i0 = (int)fminf(fmaxf(i0f, 0.0f), (float)(W - 1)), i1 = (int)fminf(fmaxf(i0f + 1.0f, 0.0f), (float)(W - 1));
-    const int j0 = (int)fminf(fmaxf(j0f, 0.0f), (float)(H - 1)), j1 = (int)fminf(fmaxf(j0f + 1.0f, 0.0f), (float)(H - 1));
+    const int i0 = (int)fminf(fmaxf(i0f, 0.0f), P.env_wf[2]), i1 = (int)fminf(fmaxf(i0f + 1.0f, 0.0f), P.env_wf[2]);
+    const int j0 = (int)fminf(fmaxf(j0f, 0.0f), P.env_wf[3]), j1 = (int)fminf(fmaxf(j0f + 1.0f, 0.0f), P.env_wf[3]);
     const float4 t00 = P.env[(size_t)j0 * W + i0], t10 = P.env[(size_t)j0 * W + i1];
     const float4 t01 = P.env[(size_t)j1 * W + i0], t11 = P.env[(size_t)j1 * W + i1];
     const float ia = 1.0f - a, ib = 1.0f - b;
@@ -1278,15 +1280,18 @@ RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& tim
 RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
     const float gxt = (float)px + time, gyt = (float)py + time;
     rc = 0.0f;
-    const float W = (float)P.W, H = (float)P.H;
+    const float W = P.Wf, H = P.Hf;   // (float)P.W, (float)P.H, converted on the host
     const float posx = (float)px / W, posy = (float)py / H;
     const float j1 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
     const float j2 = rand_step(gxt, gyt, rc, v2((float)px + time, (float)py + time));
     const float j3 = rand_step(gxt, gyt, rc, v2((float)py + time, (float)px + time));
-    const V3 r00 = v3(P.r00[0], P.r00[1], P.r00[2]), r01 = v3(P.r01[0], P.r01[1], P.r01[2]);
-    const V3 r10 = v3(P.r10[0], P.r10[1], P.r10[2]), r11 = v3(P.r11[0], P.r11[1], P.r11[2]);
-    const V3 top = vmix(r00, r01, posx + j1 / W);
-    const V3 bot = vmix(r10, r11, posx + j2 / W);
+    // mix(r00, r01, x) = fma(x, r01 - r00, r00) (rmr_math.h fmix): the differences r01 - r00 and
+    // r11 - r10 come from the host (the same float subtraction; scalar operands here instead of
+    // hoisted VGPRs the allocator spilled)
+    const V3 r00 = v3(P.r00[0], P.r00[1], P.r00[2]), r10 = v3(P.r10[0], P.r10[1], P.r10[2]);
+    const V3 d0 = v3(P.dr01[0], P.dr01[1], P.dr01[2]), d1 = v3(P.dr11[0], P.dr11[1], P.dr11[2]);
+    const V3 top = vfma(d0, posx + j1 / W, r00);
+    const V3 bot = vfma(d1, posx + j2 / W, r10);
     return normalize(vmix(top, bot, posy + j3 / H));
 }
 
@@ -1438,9 +1443,12 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 // cert / w (HO kernels whose map certifies its minimiser, MAP::kCert): a hit whose getNormal probes
 // all have primitive w as their unique minimiser (am_normal_cert) skips the six probe iterations: it
 // parks in PH_HIT with ctr = -1, and the shading batch evaluates the probes on w alone
-// (normal_from_prim), the same six map() values
+// (cert_normals), the same six map() values
+// p (cache kernels with one cached primitive): the march point, for the same certificate from the
+// cache's bound — a hit whose six probes all stay within the cached primitive's validity (each probe
+// would be served by the cache, F_w(probe) < cs - delta - eps) parks in PH_HIT with ctr = -1 too
 template <bool HO, bool CACHE = false>
-RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = false) {
+RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = false, V3 p = V3{0.0f, 0.0f, 0.0f}) {
     if constexpr (HO && !CACHE) {   // (cache kernels: A/B neutral-negative)
         // HO kernels (no shadow rays): the same state transitions as below as per-lane selects
         const float dist = L.inside ? -m.x : m.x;
@@ -1465,12 +1473,25 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = 
         if (shadow) {          // sd = t; keep hit/mid/normal of the shaded point
             L.phase = PH_NEE;
         } else {
-            if constexpr (CACHE) L.cs -= (L.t - L.cta) * (1.0f + 0x1p-21f);   // cache now relative to the hit
+            bool c = false;
+            if constexpr (CACHE) {
+                L.cs -= (L.t - L.cta) * (1.0f + 0x1p-21f);   // cache now relative to the hit
+                if constexpr (HO && RMR_NPC_K == 1) {
+                    // every probe q is served by the cache when F_w(q) < cs - delta - eps(q); with
+                    // F_w(q) <= F_w(p) + delta + 2 eps (1-Lipschitz, float error; F_w(p) = m.x, the
+                    // cached or re-anchored minimiser's distance: cs = -inf without one) and eps the
+                    // npc_eps bound over the probes' box: cs - 2 delta - 3 eps > m.x, with |cs| 2^-20 for
+                    // this test's rounding (NaN / -inf: false)
+                    const float ax = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
+                    const float eps = fmaf(ax + 0.002f, 0x1p-17f, P.npc_eps0);
+                    c = L.cs - fmaf(fabsf(L.cs), 0x1p-20f, fmaf(3.0f, eps, 2.0f * NPC_PROBE_DELTA)) > m.x;
+                }
+            }
             L.mid = m.y;
-            if constexpr (HO) L.e = v3(0.001f, 0.0f, 0.0f);   // first probe (init_probe)
+            if constexpr (HO) L.e = c ? L.e : v3(0.001f, 0.0f, 0.0f);   // first probe (init_probe)
             else hitref<HO>(L) = vfma(L.d, L.t, L.o);
-            L.ctr = 0;
-            L.phase = PH_NORMAL;
+            L.ctr = c ? -1 : 0;
+            L.phase = c ? PH_HIT : PH_NORMAL;
         }
         return;
     }
@@ -1533,27 +1554,53 @@ RMR_D void normal_update(Lane& L, float m) {
     if (L.ctr == 6) L.phase = PH_HIT;   // normalize() happens in the shading batch (shade())
 }
 
-// getNormal (RM1:259-268) of a hit certified by its march_update (cert, w): the six probes hp + e_c
-// with normal_update's offsets and signed zeros, each probe's map() = opU((maxDist, -1), F_w(probe),
-// id_w) whose distance is F_w (or maxDist beyond it); F_w by prim_dist_at, bit-identical to sd_box /
-// sd_sphere at points without NaN (the hit point is finite: am_normal_cert). One per-lane table read
-// of the primitive for the six.
-RMR_D V3 normal_from_prim(const KParams& P, V3 hp, int w) {
-    const float4* q = (const float4*)(P.dprims + w);
-    const float4 qa = q[0], qb = q[1];
-    const float4 pr[2] = {qa, qb};
-    const float h = 0.001f;
-    float mv[6];
-    V3 e = v3(h, 0.0f, 0.0f);
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
+// getNormal (RM1:259-268) of the hits certified by their march_update (cert, w; ctr = -1), at the
+// shading batch and spread over the whole wave (ballot / prefix compaction): probe c of the certified
+// lane of rank r (among the certified lanes, mbcnt) is evaluation g = 6 r + c, run by lane g mod 64 in
+// pass g / 64, so a batch of n certified hits costs ceil(6 n / 64) evaluations per lane instead of six.
+// The helper lane fetches the owner's hit point and primitive with ds_bpermute (the owner's lane from
+// a per-wave LDS table of ranks), evaluates the probe hp + e_c (normal_update's offsets and signed
+// zeros) on that primitive alone — each probe's map() is opU((maxDist, -1), F_w(probe), id_w) by the
+// certificate, distance F_w or maxDist beyond it; F_w by prim_dist_at, bit-identical to sd_box /
+// sd_sphere at points without NaN — and each owner gathers its six values back with ds_bpermute:
+// nrm = (m0 - m1, m2 - m3, m4 - m5), normalised in shade() as every normal.
+// Runs with every lane of the wave active (bpermute reads the owners' registers).
+RMR_D void cert_normals(const KParams& P, Lane& L, bool mine, uint64_t cm, int* tab, const float4* dtab) {
+    const int lane = (int)__lane_id();
+    const int n = __popcll(cm);
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+    if (mine) tab[rank] = lane;
+    __builtin_amdgcn_wave_barrier();
+    const V3 hp = vfma(L.d, L.t, L.o);   // the hit point (HO: written at the shading batch, same bits)
+    const int total = 6 * n;
+    float v[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int g0 = 0; g0 < total; g0 += 64) {   // wave-uniform
+        const int g = g0 + lane;
+        const bool act = g < total;
+        const int r = act ? g / 6 : 0;
+        const int c = g - 6 * r;
+        const int own = tab[r];
+        const float hx = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * own, __float_as_int(hp.x)));
+        const float hy = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * own, __float_as_int(hp.y)));
+        const float hz = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * own, __float_as_int(hp.z)));
+        const int w = __builtin_amdgcn_ds_bpermute(4 * own, L.cw);
+        // e_c: (+h,+0,+0) (-h,-0,-0) (+0,+h,+0) (-0,-h,-0) (+0,+0,+h) (-0,-0,-h)
+        const float sg = (c & 1) ? -1.0f : 1.0f;
+        const int ax = c >> 1;
+        const V3 e = v3(sg * (ax == 0 ? 0.001f : 0.0f), sg * (ax == 1 ? 0.001f : 0.0f), sg * (ax == 2 ? 0.001f : 0.0f));
         float mid;
         int j;
-        const float F = prim_dist_at(pr, hp + e, mid, j);
-        mv[c] = (P.max_dist >= F) ? F : P.max_dist;   // opu(d = (maxDist, -1), F, .).x
-        e = (c & 1) == 0 ? -e : v3(-e.z, -e.x, -e.y);   // normal_update's cycle
+        const float F = prim_dist_at(dtab + 2 * (act ? w : 0), v3(hx, hy, hz) + e, mid, j);
+        const float val = (P.max_dist >= F) ? F : P.max_dist;   // opu(d = (maxDist, -1), F, .).x
+#pragma unroll
+        for (int k = 0; k < 6; k++) {   // owners collect the values of this pass
+            const int gk = 6 * rank + k;
+            const float got = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * (gk & 63), __float_as_int(val)));
+            if (mine && (gk >> 6) == (g0 >> 6)) v[k] = got;
+        }
     }
-    return v3(mv[0] - mv[1], mv[2] - mv[3], mv[4] - mv[5]);
+    __builtin_amdgcn_wave_barrier();   // (tab is rewritten by the next batch)
+    if (mine) L.nrm = v3(v[0] - v[1], v[2] - v[3], v[4] - v[5]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1810,10 +1857,7 @@ RMR_D bool spectral_event(Lane& L, uint32_t mn, uint32_t mx, float pw, V2 seed) 
 template <int VAR, bool PROG, class MATS, bool CERT = false>
 RMR_D void shade(const KParams& P, Lane& L) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
-    // certified hits (march_update cert, ctr = -1): getNormal's probes on the hit's primitive alone
-    if constexpr (HO && CERT) {
-        if (L.phase == PH_HIT && L.ctr < 0) L.nrm = normal_from_prim(P, hitref<HO>(L), L.cw);
-    }
+    // (certified hits, CERT: L.nrm holds getNormal's differences from cert_normals)
     // getNormal's normalize (RM1:267), deferred from the last probe to the batch: the map loop then
     // carries no division/sqrt for the few lanes that finish a normal in a given iteration
     if (L.phase == PH_HIT) L.nrm = normalize(L.nrm);
@@ -2028,6 +2072,9 @@ typedef uint32_t WCount;
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
+    // certified hits (march_update: ctr = -1) get getNormal's probes in the shading batch from one
+    // primitive: the approximate sphere/box maps' certificate (MAP::kCert), the one-primitive cache's
+    constexpr bool CERT = HO && (MAP::kCert || (MAP::kCache && RMR_NPC_K == 1));
     Lane L;
     L.phase = PH_IDLE;
     init_probe(L);
@@ -2071,6 +2118,7 @@ RMR_D void trace_main(const KParams& P) {
 #define RMR_STAMP(v)
 #endif
     __shared__ ChunkRay s_ray[4][CHUNK];   // per wave (256-thread blocks = 4 waves)
+    __shared__ int s_tab[4][CERT ? 64 : 1];   // cert_normals: certified lanes by rank
     // cache kernels: the lane's shading-only state during the inner march loop (cold_put / cold_get)
     constexpr bool kStash = MAP::kCache && HO;
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
@@ -2256,7 +2304,7 @@ RMR_D void trace_main(const KParams& P) {
 #endif
                 if (done) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                    else march_update<HO, true>(P, L, m);
+                    else march_update<HO, true>(P, L, m, 0, false, p);
                 }
                 const uint64_t dm = __ballot(done);
                 maps += (WCount)__popcll(dm);
@@ -2341,8 +2389,10 @@ RMR_D void trace_main(const KParams& P) {
         if (smask && (__popcll(smask) >= T || amask2 == 0)) {
             shades++;
             shaded += (WCount)__popcll(smask);
-            if constexpr (MAP::kCert && HO) {   // the certified hits' probes (shade: normal_from_prim)
-                const uint64_t cm = __ballot(L.phase == PH_HIT && L.ctr < 0);
+            if constexpr (CERT) {   // the certified hits' getNormal probes, spread over the wave
+                const bool mine = L.phase == PH_HIT && L.ctr < 0;
+                const uint64_t cm = __ballot(mine);
+                if (cm) cert_normals(P, L, mine, cm, s_tab[wv], RMR_DTAB);
                 maps += (WCount)(6 * __popcll(cm));
                 bmaps += (WCount)(6 * __popcll(cm));
 #ifdef RMR_COUNT_FLOPS
@@ -2357,7 +2407,7 @@ RMR_D void trace_main(const KParams& P) {
                     L.o = vfma(L.d, L.t, L.o);
                     L.e = v3s(-0.0f);
                 }
-                shade<VAR, PROG, MATS, MAP::kCert && HO>(P, L);
+                shade<VAR, PROG, MATS, CERT>(P, L);
             }
         }
         // finished samples have stored their radiance (finish_trace): the lane is free
@@ -2380,7 +2430,7 @@ RMR_D void trace_main(const KParams& P) {
                 if (MAP::kCache) atomicAdd(P.counters + 3, (unsigned long long)fulls);   // full map() batches
                 atomicAdd(P.counters + 8, (unsigned long long)shaded);   // lane-level shading events
                 // map() evaluations of the shading batches (certified getNormal probes; in [0] too)
-                if (MAP::kCert && HO) atomicAdd(P.counters + 14, (unsigned long long)bmaps);
+                if (CERT) atomicAdd(P.counters + 14, (unsigned long long)bmaps);
             }
             maps = iters = shades = fulls = shaded = bmaps = 0;
         }
