@@ -1444,6 +1444,9 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
 // all have primitive w as their unique minimiser (am_normal_cert) skips the six probe iterations: it
 // parks in PH_HIT with ctr = -1, and the shading batch evaluates the probes on w alone
 // (cert_normals), the same six map() values
+#ifndef RMR_CACHE_CERT
+#define RMR_CACHE_CERT 1   // (0: the cache kernels probe in the march loop, A/B)
+#endif
 // p (cache kernels with one cached primitive): the march point, for the same certificate from the
 // cache's bound — a hit whose six probes all stay within the cached primitive's validity (each probe
 // would be served by the cache, F_w(probe) < cs - delta - eps) parks in PH_HIT with ctr = -1 too
@@ -1476,7 +1479,7 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = 
             bool c = false;
             if constexpr (CACHE) {
                 L.cs -= (L.t - L.cta) * (1.0f + 0x1p-21f);   // cache now relative to the hit
-                if constexpr (HO && RMR_NPC_K == 1) {
+                if constexpr (HO && RMR_NPC_K == 1 && RMR_CACHE_CERT) {
                     // every probe q is served by the cache when F_w(q) < cs - delta - eps(q); with
                     // F_w(q) <= F_w(p) + delta + 2 eps (1-Lipschitz, float error; F_w(p) = m.x, the
                     // cached or re-anchored minimiser's distance: cs = -inf without one) and eps the
@@ -2054,9 +2057,14 @@ RMR_D bool is_shade(int ph) { return ph >= PH_HIT; }   // (PH_DONE, -1, is not)
 #ifndef RMR_PROG_WAVES
 #define RMR_PROG_WAVES 1
 #endif
+// waves/SIMD target of the RM2 (next-event estimation) kernels: 1 = the allocator's choice (5 waves)
+#ifndef RMR_RM2_WAVES
+#define RMR_RM2_WAVES 1
+#endif
 template <int VAR, bool GENERAL, bool PROG>
 constexpr int trace_waves() {
-    return PROG ? RMR_PROG_WAVES : (VAR == RMR_VARIANT_RM2 ? 1 : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES));
+    return PROG ? RMR_PROG_WAVES
+                : (VAR == RMR_VARIANT_RM2 ? RMR_RM2_WAVES : (GENERAL ? RMR_GENERAL_WAVES : RMR_FAST_WAVES));
 }
 
 // the map() point of an active lane: one select per component in HO kernels (A/B: C2 +1%; the RM2
@@ -2074,7 +2082,7 @@ RMR_D void trace_main(const KParams& P) {
     constexpr bool HO = hit_in_origin<VAR, PROG>();
     // certified hits (march_update: ctr = -1) get getNormal's probes in the shading batch from one
     // primitive: the approximate sphere/box maps' certificate (MAP::kCert), the one-primitive cache's
-    constexpr bool CERT = HO && (MAP::kCert || (MAP::kCache && RMR_NPC_K == 1));
+    constexpr bool CERT = HO && (MAP::kCert || (MAP::kCache && RMR_NPC_K == 1 && RMR_CACHE_CERT));
     Lane L;
     L.phase = PH_IDLE;
     init_probe(L);

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-4 measurements in one GPU call (diagnostic library; logs in gpurun_out/r04ab_*.log):
+# RM2's drain and section cycles, the C2 shading threshold, the certified getNormal probes on / off
+# (C2's approximate map, C4's cache), RM2 and cache-kernel wave targets.
+export RMR_LIB=diag
+cd "$(dirname "$0")/.." || exit 2
+mkdir -p gpurun_out
+run() {   # name, command...
+  local n=$1; shift
+  timeout -k 10 400 "$@" > "gpurun_out/r04ab_$n.log" 2>&1 || return $?
+  echo "== $n"; grep -v "amdgpu.ids" "gpurun_out/r04ab_$n.log" | tail -6
+}
+S=tests/golden/scenes/simple.scene
+run rm2_wave_times python -u tools/wave_times.py --variant rm2 --scene $S --bounces 16 --spp 4,16,64 || exit $?
+RMR_JIT_OPTS=-DRMR_PROFILE run rm2_sections python -u tools/stats_run.py --variant rm2 --scene $S --bounces 16 --spp 4 || exit $?
+run c2_cert python -u tools/env_ab.py RMR_JIT_CERT 1 0 --scenes cornell5 --rounds 5 --spp 16 || exit $?
+run c4_cert python -u tools/env_ab.py RMR_JIT_OPTS "" "-DRMR_CACHE_CERT=0" --scenes csg256 --rounds 4 --spp 8 || exit $?
+run rm2_waves python -u tools/env_ab.py RMR_JIT_OPTS "" "-DRMR_RM2_WAVES=6" "-DRMR_RM2_WAVES=8" --scenes rm2simple --rounds 4 --spp 16 || exit $?
+run c2_shade_t python -u tools/env_ab.py shade_t 12 14 16 20 --scenes cornell5 --rounds 3 --spp 16 || exit $?
+exit 0

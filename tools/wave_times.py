@@ -17,10 +17,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--spp", default="8,64")
 ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "cornell5.scene"))
 ap.add_argument("--bounces", type=int, default=4)
+ap.add_argument("--variant", default="rm1", help="rm1 / rm2 / rm3 (rm3: --scene builtin)")
 a = ap.parse_args()
 r = Renderer(0, 1920, 1080)
 r.set_jit(1)
-r.load_scene(a.scene, "rm1")
+if a.scene == "builtin":
+    r.load_builtin(a.variant)
+else:
+    r.load_scene(a.scene, a.variant)
 r.set_params(abi.default_params(max_bounces=a.bounces))
 r.reload()
 r.render_spp(time_schedule(2))
