@@ -791,6 +791,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.Wf = (float)c->W; P.Hf = (float)c->H;
     P.env_wf[0] = (float)c->env_w; P.env_wf[1] = (float)c->env_h;
     P.env_wf[2] = (float)(c->env_w - 1); P.env_wf[3] = (float)(c->env_h - 1);
+    P.eye_xy = P.eye[0] + P.eye[1];
     P.x0 = x0; P.y0 = y0; P.x1 = x1; P.y1 = y1;
     P.tiles = c->d_tiles;
     P.n_tiles = (int)tiles.size();

@@ -104,6 +104,7 @@ struct KParams {
     float dr01[3], dr11[3];
     float Wf, Hf;
     float env_wf[4];
+    float eye_xy;               // eye.x + eye.y (the first sum of a primary ray's ray_exit NaN check)
     // ---- work ----
     int32_t x0, y0, x1, y1;     // clip rect (pixels inside = rendered)
     const TileXY* tiles;        // n_tiles tiles

@@ -1196,8 +1196,10 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
 // which the NaN-dropping fminf/fmaxf ignore (the ray then lies on a box face: >= the inflation
 // from every primitive). A NaN origin or direction (e.g. randHemisphere about a normal of exactly
 // (0,-1,0)) never escapes: the reference's map(NaN) "hits" at t = 0 (opU NaN rule).
-RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
-    const float chk = ((o.x + o.y) + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
+// (oxy = o.x + o.y: primary rays pass the host's P.eye_xy, a value the kernel would otherwise keep in a
+// VGPR for the whole launch)
+RMR_D float ray_exit(const KParams& P, V3 o, V3 d, float oxy) {
+    const float chk = (oxy + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
     if (!P.esc_on || !(chk == chk)) return __builtin_inff();
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     float last = -__builtin_inff();
@@ -1216,9 +1218,13 @@ RMR_D float ray_exit(const KParams& P, V3 o, V3 d) {
     // relative error < 2^-21: widen a positive bound
     return last > 0.0f ? fmaf(last, 1.0f + 0x1p-19f, 0x1p-60f) : last;
 }
+RMR_D float ray_exit(const KParams& P, V3 o, V3 d) { return ray_exit(P, o, d, o.x + o.y); }
 
 // te_pre: the ray's escape bound when the caller has it (primary rays: computed full-width with the
-// chunk's rays, chunk_ray); NaN = compute it here
+// chunk's rays, chunk_ray; RM2's shadow rays: with the light-side bound); NaN = compute it here
+#ifndef RMR_SHADOW_LIGHT_BOUND
+#define RMR_SHADOW_LIGHT_BOUND 1   // (0: shadow rays with the escape bound alone, A/B)
+#endif
 template <bool HO>
 RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
     L.t = 0.0f;
@@ -1326,6 +1332,9 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
             return true;
         }
         if (L.chan < 0) {
+#ifdef RMR_DIAG_NO_STORE   // timing experiment only (wrong planes): what the plane stores cost
+            if (res.x == -1234.5f)
+#endif
             P.samp[L.unit] = make_float4(res.x, res.y, res.z, 1.0f);
             return true;
         }
@@ -1406,7 +1415,7 @@ RMR_D ChunkRay chunk_ray(const KParams& P, uint32_t u) {
     float te = __builtin_nanf("");
     if (in_rect) {
         dir = primary_dir(P, px, py, time, rc);
-        te = ray_exit(P, v3(P.eye[0], P.eye[1], P.eye[2]), dir);   // never NaN
+        te = ray_exit(P, v3(P.eye[0], P.eye[1], P.eye[2]), dir, P.eye_xy);   // never NaN
     }
     r.a = make_float4(dir.x, dir.y, dir.z, rc);
     r.b = make_float4((float)px + time, (float)py + time, time, te);
@@ -1929,7 +1938,19 @@ RMR_D void shade(const KParams& P, Lane& L) {
             } else {  // light-march toward the point light, RM2:481
                 L.o = vfma(N, 0.002f, pos);
                 L.d = normalize(lp - pos);
-                start_march<HO>(P, L, PH_SHADOW);   // hit/mid/nrm stay for the NEE step
+                // Light-side bound: the NEE step reads this march only through sd >= len (RM2:482,
+                // len = length(lightPos - pos), the same expression as there). t starts at 0 <= len and
+                // a step adds dist * stepMultiply with dist >= 0.001, so t can pass len only with
+                // stepMultiply > 0, and then never decreases: every ending after that gives sd >= len (a
+                // hit returns its t > len; a miss or the step limit maxDist >= len). The march may then
+                // end as its miss at once (t = maxDist), as past the escape bound; only the number of
+                // map() calls differs.
+                float te = __builtin_nanf("");   // (start_march: the escape bound alone)
+#if RMR_SHADOW_LIGHT_BOUND
+                const float len = length(lp - pos);
+                if (P.esc_on && len <= P.max_dist) te = fminf(ray_exit(P, L.o, L.d), len);
+#endif
+                start_march<HO>(P, L, PH_SHADOW, te);   // hit/mid/nrm stay for the NEE step
             }
         } else if (L.phase == PH_NEE) {  // RM2:482-501
             const V3 pos = hitref<HO>(L), N = L.nrm;
@@ -2024,6 +2045,15 @@ RMR_D void cold_get(float (*s)[256], int t, Lane& L) {
     const int cb = __float_as_int(s[7][t]);
     L.chan = (cb & 0xff) - 1;
     L.bounces = cb >> 8;
+}
+
+// The lane id where trace_main needs it (the work-queue fetch, counter flushes): recomputed at each
+// use (two VALU) instead of a hoisted value the allocator keeps across the loop — at 8 waves / SIMD it
+// spilled that register to scratch (the stepped Mandelbulb kernel)
+RMR_D uint32_t lane_now() {
+    uint32_t v;
+    __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
 }
 
 RMR_D bool is_active(int ph) { return (uint32_t)ph <= (uint32_t)PH_SHADOW; }   // PH_DONE (-1) is not
@@ -2132,6 +2162,14 @@ RMR_D void trace_main(const KParams& P) {
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
+    // the stepped Mandelbulb kernel (8 waves / SIMD, 20 KiB of LDS per block): the RNG seeds gx + time,
+    // gy + time, which only shading reads, wait in LDS from the unit's start instead of in registers
+    // the allocator spilled to scratch
+#ifndef RMR_SEED_LDS
+#define RMR_SEED_LDS 1
+#endif
+    constexpr bool kSeeds = MAP::kStepped && PERSIST && RMR_SEED_LDS;
+    __shared__ float s_seed[kSeeds ? 2 : 1][4][kSeeds ? 64 : 1];
     const bool dp_lds = MAP::kCache && P.n_prims <= RMR_NPC_LDS_MAX;
     if (dp_lds) {
         for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
@@ -2139,12 +2177,12 @@ RMR_D void trace_main(const KParams& P) {
     }
 #define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_at(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
 #define RMR_DTAB (dp_lds ? (const float4*)s_dp : (const float4*)P.dprims)
-    const int wv = (threadIdx.x >> 6) & 3;
+    const int wv = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);   // the wave's index in its block (an SGPR)
     uint32_t chunk_base = 0;
 #ifdef RMR_WAVE_TIMES   // counters [9] ~min start, [11] ~min / [10] max queue exhaustion, [12] ~min /
                         // [13] max end, [15] sum over waves of end - exhaustion (s_memrealtime ticks)
     unsigned long long t_exh = 0;
-    if (__lane_id() == 0) atomicMax(P.counters + 9, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (lane_now() == 0) atomicMax(P.counters + 9, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
     for (;;) {
         RMR_STAMP(c0);
@@ -2156,13 +2194,13 @@ RMR_D void trace_main(const KParams& P) {
             if (idle && (__popcll(idle) >= TR || act0 == 0)) {
                 if (rnext >= rend) {
                     unsigned int base = 0;
-                    if (__lane_id() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK);
+                    if (lane_now() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK);
                     base = __builtin_amdgcn_readfirstlane(base);
                     rnext = base;
                     exhausted = base >= n_units;
                     rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
 #ifdef RMR_WAVE_TIMES   // diagnostics (tools/wave_times.py): when each wave finds the queue empty
-                    if (exhausted && __lane_id() == 0) {
+                    if (exhausted && lane_now() == 0) {
                         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
                         t_exh = te;
                         atomicMax(P.counters + 11, ~te);
@@ -2171,7 +2209,7 @@ RMR_D void trace_main(const KParams& P) {
 #endif
                     if (!exhausted) {  // the chunk's primary rays, all 64 lanes at once
                         chunk_base = base;
-                        for (uint32_t sl = __lane_id(); sl < CHUNK; sl += 64) {
+                        for (uint32_t sl = lane_now(); sl < CHUNK; sl += 64) {
                             if (base + sl < rend) s_ray[wv][sl] = chunk_ray<HO>(P, base + sl);
                         }
                         __builtin_amdgcn_wave_barrier();
@@ -2196,6 +2234,11 @@ RMR_D void trace_main(const KParams& P) {
             if (__ballot(fresh)) {
                 if (fresh) {
                     const ChunkRay cr = s_ray[wv][fu - chunk_base];
+                    if constexpr (kSeeds) {
+                        const uint32_t ln = lane_now();
+                        s_seed[0][wv][ln] = cr.b.x;
+                        s_seed[1][wv][ln] = cr.b.y;
+                    }
                     begin_unit<VAR, HO>(P, L, fu, cr.a, cr.b);
                 }
             }
@@ -2411,6 +2454,11 @@ RMR_D void trace_main(const KParams& P) {
 #endif
             }
             if (is_shade(L.phase)) {
+                if constexpr (kSeeds) {
+                    const uint32_t ln = lane_now();
+                    L.gxt = s_seed[0][wv][ln];
+                    L.gyt = s_seed[1][wv][ln];
+                }
                 if constexpr (HO) {   // the finished march's point (init_probe); the next march's e
                     L.o = vfma(L.d, L.t, L.o);
                     L.e = v3s(-0.0f);
@@ -2431,7 +2479,7 @@ RMR_D void trace_main(const KParams& P) {
         // (an inner loop adds at most 64 x its iterations to `maps`; a flush every 2^30 keeps every
         // 32-bit counter far from wrapping between two checks)
         if (last || ((maps | shaded) >> 30) != 0) {
-            if (__lane_id() == 0) {
+            if (lane_now() == 0) {
                 atomicAdd(P.counters + 0, (unsigned long long)maps);     // lane-level map() evaluations
                 atomicAdd(P.counters + 1, (unsigned long long)iters);    // wave-level map() iterations
                 atomicAdd(P.counters + 2, (unsigned long long)shades);   // wave-level shading batches
@@ -2445,14 +2493,14 @@ RMR_D void trace_main(const KParams& P) {
         if (last) break;
     }
 #ifdef RMR_WAVE_TIMES
-    if (__lane_id() == 0) {
+    if (lane_now() == 0) {
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
         atomicMax(P.counters + 12, ~tn);
         atomicMax(P.counters + 13, tn);
         if (t_exh) atomicAdd(P.counters + 15, tn - t_exh);
     }
 #endif
-    if (__lane_id() == 0) {
+    if (lane_now() == 0) {
 #ifdef RMR_PROFILE
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);
