@@ -1226,16 +1226,10 @@ RMR_D float ray_exit(const KParams& P, V3 o, V3 d) { return ray_exit(P, o, d, o.
 #define RMR_SHADOW_LIGHT_BOUND 1   // (0: shadow rays with the escape bound alone, A/B)
 #endif
 template <bool HO>
-RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
+RMR_D void start_march_te(const KParams& P, Lane& L, int phase_on_run, float texit) {
     L.t = 0.0f;
     L.ctr = 0;
-    // every march from outside (primary, bounce, RM2's shadow rays) gets its escape bound; past it
-    // the march can only end as its miss, whose state (t = maxDist) is the same whichever step
-    // reaches it. An inside march (distMult = -1, RM1:498-505) does not: past its object's box the
-    // reference's next map() is positive, -map < 0.001, a hit — which a step longer than the distance
-    // to the surface (stepMultiply > 1) can reach in one step from inside
-    const bool inside_march = L.inside && phase_on_run != PH_SHADOW;
-    L.texit = (te_pre == te_pre) ? te_pre : (inside_march ? __builtin_inff() : ray_exit(P, L.o, L.d));
+    L.texit = texit;
     if (P.max_steps > 0 && !(L.texit < 0.0f)) {
         L.phase = phase_on_run;
     } else if (phase_on_run == PH_SHADOW) {  // march() falls out of its loop: miss
@@ -1247,6 +1241,17 @@ RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre
         if constexpr (!HO) hitref<HO>(L) = vfma(L.d, L.t, L.o);   // (HO: written at the shading batch)
         L.phase = PH_MISS;
     }
+}
+// every march from outside (primary, bounce, RM2's shadow rays) gets its escape bound; past it the
+// march can only end as its miss, whose state (t = maxDist) is the same whichever step reaches it. An
+// inside march (distMult = -1, RM1:498-505) does not: past its object's box the reference's next map()
+// is positive, -map < 0.001, a hit — which a step longer than the distance to the surface
+// (stepMultiply > 1) can reach in one step from inside
+template <bool HO>
+RMR_D void start_march(const KParams& P, Lane& L, int phase_on_run, float te_pre = __builtin_nanf("")) {
+    const bool inside_march = L.inside && phase_on_run != PH_SHADOW;
+    start_march_te<HO>(P, L, phase_on_run,
+                       (te_pre == te_pre) ? te_pre : (inside_march ? __builtin_inff() : ray_exit(P, L.o, L.d)));
 }
 
 // trace() prologue: o = eye, d = dir, per-variant throughput init (RM1:485-492, RM2:422-429,
@@ -1262,7 +1267,8 @@ RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir, float te_pre = __bu
     if (VAR == RMR_VARIANT_RM3) { L.wl = 0u; L.power = 1.0f; }
     if (L.bounces < P.max_bounces) {
         L.bounces = 1;
-        start_march<HO>(P, L, PH_MARCH, te_pre);
+        // a primary ray's escape bound from the eye (o.x + o.y = the host's eye_xy, the same bits)
+        start_march_te<HO>(P, L, PH_MARCH, (te_pre == te_pre) ? te_pre : ray_exit(P, L.o, dir, P.eye_xy));
         return true;
     }
     return false;
@@ -1464,12 +1470,13 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = 
     if constexpr (HO && !CACHE) {   // (cache kernels: A/B neutral-negative)
         // HO kernels (no shadow rays): the same state transitions as below as per-lane selects
         const float dist = L.inside ? -m.x : m.x;
-        const bool hit = dist < 0.001f;
+        const bool hit0 = dist < 0.001f;
+        const bool hit = hit0 && (L.t < P.max_dist);   // a far hit is trace()'s miss (see below)
         const bool past = L.t >= P.max_dist;
         const float tn = fmaf(dist, P.step_mult, L.t);
         const int cn = L.ctr + 1;
-        const bool miss = !hit && (past || cn >= P.max_steps || tn > L.texit);
-        const float tf = hit ? L.t : (miss ? P.max_dist : tn);
+        const bool miss = hit0 ? !hit : (past || cn >= P.max_steps || tn > L.texit);
+        const float tf = hit0 ? L.t : (miss ? P.max_dist : tn);
         const bool probe = hit && !cert;
         L.t = tf;   // (o stays the ray origin: the shading batch writes the point, init_probe)
         L.e = v3(probe ? 0.001f : L.e.x, probe ? 0.0f : L.e.y, probe ? 0.0f : L.e.z);
@@ -1484,6 +1491,14 @@ RMR_D void march_update(const KParams& P, Lane& L, V2 m, int w = 0, bool cert = 
     if (dist < 0.001f) {
         if (shadow) {          // sd = t; keep hit/mid/normal of the shaded point
             L.phase = PH_NEE;
+        } else if (!(L.t < P.max_dist)) {
+            // A far hit: march() returns its t as a hit even at t >= maxDist (its hit test comes
+            // before the t >= maxDist test, RM1:240-251) — a step of stepMultiply > 1 can overshoot
+            // into an object there — but trace() shades only `v.x < maxDist` (RM1:514, RM2:436,
+            // RM3:368); otherwise its miss branch runs, with the point o + t d (RM3's rand seed)
+            L.mid = -1.0f;
+            if constexpr (!HO) hitref<HO>(L) = vfma(L.d, L.t, L.o);
+            L.phase = PH_MISS;
         } else {
             bool c = false;
             if constexpr (CACHE) {
@@ -2162,14 +2177,14 @@ RMR_D void trace_main(const KParams& P) {
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
-    // the stepped Mandelbulb kernel (8 waves / SIMD, 20 KiB of LDS per block): the RNG seeds gx + time,
-    // gy + time, which only shading reads, wait in LDS from the unit's start instead of in registers
-    // the allocator spilled to scratch
+    // the stepped Mandelbulb kernel (8 waves / SIMD, 20 KiB of LDS per block): the RNG state (seeds
+    // gx + time, gy + time and the chain value randChange), which only shading reads and advances,
+    // waits in LDS between shading batches instead of in registers the allocator spilled to scratch
 #ifndef RMR_SEED_LDS
 #define RMR_SEED_LDS 1
 #endif
     constexpr bool kSeeds = MAP::kStepped && PERSIST && RMR_SEED_LDS;
-    __shared__ float s_seed[kSeeds ? 2 : 1][4][kSeeds ? 64 : 1];
+    __shared__ float s_rng[kSeeds ? 3 : 1][4][kSeeds ? 64 : 1];
     const bool dp_lds = MAP::kCache && P.n_prims <= RMR_NPC_LDS_MAX;
     if (dp_lds) {
         for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
@@ -2236,8 +2251,9 @@ RMR_D void trace_main(const KParams& P) {
                     const ChunkRay cr = s_ray[wv][fu - chunk_base];
                     if constexpr (kSeeds) {
                         const uint32_t ln = lane_now();
-                        s_seed[0][wv][ln] = cr.b.x;
-                        s_seed[1][wv][ln] = cr.b.y;
+                        s_rng[0][wv][ln] = cr.b.x;
+                        s_rng[1][wv][ln] = cr.b.y;
+                        s_rng[2][wv][ln] = cr.a.w;
                     }
                     begin_unit<VAR, HO>(P, L, fu, cr.a, cr.b);
                 }
@@ -2454,16 +2470,19 @@ RMR_D void trace_main(const KParams& P) {
 #endif
             }
             if (is_shade(L.phase)) {
+                uint32_t ln = 0;
                 if constexpr (kSeeds) {
-                    const uint32_t ln = lane_now();
-                    L.gxt = s_seed[0][wv][ln];
-                    L.gyt = s_seed[1][wv][ln];
+                    ln = lane_now();
+                    L.gxt = s_rng[0][wv][ln];
+                    L.gyt = s_rng[1][wv][ln];
+                    L.rc = s_rng[2][wv][ln];
                 }
                 if constexpr (HO) {   // the finished march's point (init_probe); the next march's e
                     L.o = vfma(L.d, L.t, L.o);
                     L.e = v3s(-0.0f);
                 }
                 shade<VAR, PROG, MATS, CERT>(P, L);
+                if constexpr (kSeeds) s_rng[2][wv][ln] = L.rc;   // the chain continues at the next hit
             }
         }
         // finished samples have stored their radiance (finish_trace): the lane is free

@@ -72,9 +72,15 @@ def test_display_device_buffer_matches_host_path():
         dev = torch.zeros((80, 100, 4), dtype=torch.uint8, device="cuda")
         s = torch.cuda.Stream()
         r.set_stream(s.cuda_stream)
-        r.display_device((50.0, 40.0), 1.5, (0, 0), (100, 80), dev.data_ptr(), 100, 80)
+        r.display_device((50.0, 40.0), 1.5, (0, 0), (100, 80), dev, 100, 80)   # a tensor: its size
         s.synchronize()
         assert np.array_equal(dev.cpu().numpy(), host)
+        dev2 = torch.zeros_like(dev)   # a raw device pointer with the buffer's size
+        r.display_device((50.0, 40.0), 1.5, (0, 0), (100, 80), dev2.data_ptr(), 100, 80, nbytes=dev2.numel())
+        s.synchronize()
+        assert np.array_equal(dev2.cpu().numpy(), host)
+        with pytest.raises(ValueError):   # a raw pointer without its size is refused (renderer.py)
+            r.display_device((50.0, 40.0), 1.5, (0, 0), (100, 80), dev2.data_ptr(), 100, 80)
     finally:
         r.close()
 

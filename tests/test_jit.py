@@ -414,6 +414,40 @@ def test_escape_bound_inside_rays_long_steps_bitexact(renderer, step_mult):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("max_dist,step_mult", [(1000.0, 0.5), (7.0, 1.0), (4.0, 1.7)])
+def test_rm2_shadow_light_bound_bitexact(renderer, max_dist, step_mult):
+    """RM2's shadow rays end at the light distance (rmr_trace.h: the NEE step reads the shadow march
+    only through sd >= length(lightPos - pos), RM2:481-482). With maxDist below some of the light
+    distances (the bound is then off for those rays) and above, and stepMultiply up to 1.7: every switch
+    on and off, JIT and table kernels, and the oracle agree bitwise."""
+    W, H = 96, 64
+    path = os.path.join(GOLDEN, "scenes", "simple.scene")
+    prm, view = _setup(renderer, path, "rm2", W, H, {"max_bounces": 6, "max_dist": max_dist,
+                                                      "step_multiply": step_mult})
+    times = time_schedule(4, frame=3)
+    out = {}
+    try:
+        for jit in (1, 0):
+            renderer.set_jit(jit)
+            for flags in (abi.CULL_ALL, 0):
+                renderer.set_culling(flags)
+                renderer.reload()
+                out[(jit, flags)] = renderer.trace_samples(times, (0, 0, W, H))
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+        renderer.set_jit(2)
+    ref = out[(0, 0)]
+    for k, img in out.items():
+        same = (img.view(np.uint32) == ref.view(np.uint32)).all(-1) | (np.isnan(img).any(-1) & np.isnan(ref).any(-1))
+        assert same.all(), "%s: %d samples differ" % (k, (~same).sum())
+    rect = (24, 16, 56, 40)
+    cpu = oracle.Oracle(_tables(path, "rm2"), prm, view, W, H).trace_samples(times, rect)
+    a, b = out[(1, abi.CULL_ALL)][:, rect[1]:rect[3], rect[0]:rect[2], :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ from the oracle" % (~same.all(-1)).sum()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene,W,H", [("cornell5.scene", 1920, 1080), ("csg256.scene", 960, 540),
                                        ("rm2:simple.scene", 1920, 1080), ("default.scene", 960, 540)])
 def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
