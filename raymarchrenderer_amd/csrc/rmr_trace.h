@@ -2118,6 +2118,9 @@ constexpr int trace_waves() {
 #ifndef RMR_CHUNK
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
+#ifndef RMR_SUPER
+#define RMR_SUPER 1   // chunks per work-queue atomic
+#endif
 #ifndef RMR_CHUNK_CACHE
 #define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
@@ -2140,6 +2143,9 @@ RMR_D void trace_main(const KParams& P) {
     constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
+    // RMR_SUPER > 1: one work-queue atomic takes RMR_SUPER chunks, which the wave then works through
+    // one by one ([sup_next, sup_end)); fewer atomics on the one counter every wave of the chip shares
+    uint32_t sup_next = 0, sup_end = 0;
     bool exhausted = false;
     if (!PERSIST) {
         const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2209,8 +2215,14 @@ RMR_D void trace_main(const KParams& P) {
             if (idle && (__popcll(idle) >= TR || act0 == 0)) {
                 if (rnext >= rend) {
                     unsigned int base = 0;
-                    if (lane_now() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK);
-                    base = __builtin_amdgcn_readfirstlane(base);
+                    if (RMR_SUPER > 1 && sup_next < sup_end) {   // the next chunk of the wave's own range
+                        base = sup_next;
+                    } else {
+                        if (lane_now() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK * RMR_SUPER);
+                        base = __builtin_amdgcn_readfirstlane(base);
+                        sup_end = base + CHUNK * RMR_SUPER;
+                    }
+                    sup_next = base + CHUNK;
                     rnext = base;
                     exhausted = base >= n_units;
                     rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);

@@ -414,6 +414,38 @@ def test_escape_bound_inside_rays_long_steps_bitexact(renderer, step_mult):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scene,max_dist", [("cornell5.scene", 6.0), ("rm3", 5.0), ("mandelbulb.scene", 2.5),
+                                            ("csg64.scene", 12.0), ("default.scene", 6.0)])
+def test_far_hits_take_the_miss_branch_bitexact(renderer, scene, max_dist):
+    """march() returns a hit's t even when t >= maxDist (its hit test precedes the t >= maxDist test,
+    RM1:240-251), and a step of stepMultiply > 1 can overshoot into an object there; trace() shades only
+    `v.x < maxDist` (RM1:514, RM2:436, RM3:368) and runs its miss branch otherwise, with the point
+    o + t d (RM3's rand seed). Every kernel class (approximate sphere/box map, RM3, stepped Mandelbulb,
+    nearest-primitive cache, node-program materials) against the oracle, culling on and off."""
+    W, H = 64, 48
+    path, variant = _cull_scene(scene)
+    prm, view = _setup(renderer, path, variant, W, H, {"max_bounces": 4, "max_dist": max_dist,
+                                                        "step_multiply": 1.7})
+    times = time_schedule(2, frame=5)
+    out = {}
+    renderer.set_jit(1)
+    try:
+        for flags in (abi.CULL_ALL, 0):
+            renderer.set_culling(flags)
+            renderer.reload()
+            out[flags] = renderer.trace_samples(times, (0, 0, W, H))
+    finally:
+        renderer.set_culling(abi.CULL_ALL)
+        renderer.set_jit(2)
+    rect = (16, 12, 48, 36)
+    cpu = oracle.Oracle(_tables(path, variant), prm, view, W, H).trace_samples(times, rect)
+    for flags, img in out.items():
+        a, b = img[:, rect[1]:rect[3], rect[0]:rect[2], :3], cpu[..., :3]
+        same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+        assert same.all(), "culling %d: %d samples differ from the oracle" % (flags, (~same.all(-1)).sum())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("max_dist,step_mult", [(1000.0, 0.5), (7.0, 1.0), (4.0, 1.7)])
 def test_rm2_shadow_light_bound_bitexact(renderer, max_dist, step_mult):
     """RM2's shadow rays end at the light distance (rmr_trace.h: the NEE step reads the shadow march
