@@ -842,7 +842,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
             P.shade_threshold = use_jit ? c->jit.shade_t : 16;
             P.refill_threshold = refill_for(c->refill_threshold, P.shade_threshold);
         }
-        HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_queue, 0, rmr::kQueueBytes, c->stream));
         EventPair ev = get_events(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
         if (use_jit) {
@@ -911,7 +911,7 @@ int rmr_create(rmr_ctx** out, int device) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RMR_E_HIP; }
     c->own_stream = true;
     rmr_default_params(&c->params);
-    if (hipMalloc((void**)&c->d_queue, sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void**)&c->d_queue, rmr::kQueueBytes) != hipSuccess ||
         hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         rmr_destroy(c);

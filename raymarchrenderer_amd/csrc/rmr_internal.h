@@ -46,6 +46,10 @@ struct BvhNode {
     int32_t pad[3];
 };
 
+// the trace kernel's work-queue counters (rmr_trace.h RMR_QUEUE_PARTS partitions, 128 B apart; room
+// for 16), zeroed before every launch
+constexpr size_t kQueueBytes = 2048;
+
 struct KParams {
     // ---- scene tables (device pointers, read-only) ----
     const rmr_prim* prims;
@@ -115,7 +119,7 @@ struct KParams {
     uint64_t n_units;           // nspp * n_tiles * 64
     float4* samp;               // [nspp][n_tiles][64] per-sample radiance
     float4* accum;              // W*H running mean
-    unsigned long long* queue;  // persistent work counter
+    unsigned long long* queue;  // persistent work counters (kQueueBytes: one per partition, 128 B apart)
     unsigned long long* counters; // [0] map evals, [1] samples traced
     int32_t flops_static;       // count builds (RMR_COUNT_FLOPS): flops of one map() fold without the
     int32_t transc_static;      //   Mandelbulb iterations, and its transcendentals (scene.cpp)

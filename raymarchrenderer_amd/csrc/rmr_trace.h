@@ -1445,7 +1445,7 @@ RMR_D void begin_unit(const KParams& P, Lane& L, uint32_t u, float4 a, float4 b)
     L.chan = (VAR != RMR_VARIANT_RM3 && P.separate_channels != 0) ? 0 : -1;
     const V3 dir = v3(a.x, a.y, a.z);
     for (;;) {  // a zero-bounce trace finishes at once (and may start the next channel)
-        if (trace_prologue<VAR, HO>(P, L, dir, HO ? b.w : __builtin_nanf(""))) return;
+        if (trace_prologue<VAR, HO>(P, L, dir, b.w)) return;   // the escape bound from chunk_ray
         if (finish_trace<VAR, HO>(P, L)) {
             L.phase = PH_DONE;
             return;
@@ -2118,9 +2118,11 @@ constexpr int trace_waves() {
 #ifndef RMR_CHUNK
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
-#ifndef RMR_SUPER
-#define RMR_SUPER 1   // chunks per work-queue atomic
+#ifndef RMR_QUEUE_PARTS
+#define RMR_QUEUE_PARTS 8   // work-queue partitions (counters), rmr_internal.h kQueueWords
 #endif
+#define RMR_QUEUE_STRIDE 32   // 32-bit words between two partition counters (128 B)
+static_assert(RMR_QUEUE_PARTS >= 1 && RMR_QUEUE_PARTS * RMR_QUEUE_STRIDE * 4 <= (int)kQueueBytes, "queue counters");
 #ifndef RMR_CHUNK_CACHE
 #define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
@@ -2143,9 +2145,17 @@ RMR_D void trace_main(const KParams& P) {
     constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
-    // RMR_SUPER > 1: one work-queue atomic takes RMR_SUPER chunks, which the wave then works through
-    // one by one ([sup_next, sup_end)); fewer atomics on the one counter every wave of the chip shares
-    uint32_t sup_next = 0, sup_end = 0;
+    // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
+    // apart): a wave starts on partition blockIdx % parts — the XCD its block was dispatched to, for
+    // the round-robin block dispatch over the 8 XCDs — and moves on to the next partition when its own
+    // is used up. One counter shared by every wave of the chip serialises its atomics: RM2's short
+    // paths fetch ~80 chunks per microsecond, and one counter held its kernel at 3.2 ms against 1.2 ms
+    // with four chunks per atomic (tools/r04_ab2.sh).
+    const uint32_t n_chunks = (n_units + CHUNK - 1) / CHUNK;
+    auto part_begin = [&](uint32_t q) -> uint32_t {   // first unit of partition q (q = parts: the end)
+        return (uint32_t)(((uint64_t)n_chunks * q) / (uint32_t)RMR_QUEUE_PARTS) * CHUNK;
+    };
+    uint32_t part = blockIdx.x % (uint32_t)RMR_QUEUE_PARTS, tried = 0;
     bool exhausted = false;
     if (!PERSIST) {
         const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2214,18 +2224,26 @@ RMR_D void trace_main(const KParams& P) {
             uint64_t act0 = __ballot(is_active(L.phase));
             if (idle && (__popcll(idle) >= TR || act0 == 0)) {
                 if (rnext >= rend) {
+                    // the next chunk of the wave's work partition, or of the next partition once that
+                    // one is used up (every partition tried: the launch's work is all handed out)
                     unsigned int base = 0;
-                    if (RMR_SUPER > 1 && sup_next < sup_end) {   // the next chunk of the wave's own range
-                        base = sup_next;
-                    } else {
-                        if (lane_now() == 0) base = atomicAdd((unsigned int*)P.queue, CHUNK * RMR_SUPER);
-                        base = __builtin_amdgcn_readfirstlane(base);
-                        sup_end = base + CHUNK * RMR_SUPER;
+                    for (;;) {
+                        const uint32_t pb = part_begin(part), pe = part_begin(part + 1);
+                        unsigned int off = 0;
+                        if (lane_now() == 0) off = atomicAdd((unsigned int*)P.queue + RMR_QUEUE_STRIDE * part, CHUNK);
+                        off = __builtin_amdgcn_readfirstlane(off);
+                        if (off < pe - pb) {
+                            base = pb + off;
+                            rend = n_units - base > CHUNK ? base + CHUNK : n_units;
+                            break;
+                        }
+                        if (++tried >= (uint32_t)RMR_QUEUE_PARTS) {
+                            exhausted = true;
+                            break;
+                        }
+                        part = part + 1 == (uint32_t)RMR_QUEUE_PARTS ? 0 : part + 1;
                     }
-                    sup_next = base + CHUNK;
                     rnext = base;
-                    exhausted = base >= n_units;
-                    rend = exhausted ? base : (n_units - base > CHUNK ? base + CHUNK : n_units);
 #ifdef RMR_WAVE_TIMES   // diagnostics (tools/wave_times.py): when each wave finds the queue empty
                     if (exhausted && lane_now() == 0) {
                         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
