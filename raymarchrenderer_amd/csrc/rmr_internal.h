@@ -47,8 +47,8 @@ struct BvhNode {
 };
 
 // the trace kernel's work-queue counters (rmr_trace.h RMR_QUEUE_PARTS partitions, 128 B apart; room
-// for 16), zeroed before every launch
-constexpr size_t kQueueBytes = 2048;
+// for 64), zeroed before every launch
+constexpr size_t kQueueBytes = 8192;
 
 struct KParams {
     // ---- scene tables (device pointers, read-only) ----

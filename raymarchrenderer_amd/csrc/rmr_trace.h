@@ -2119,7 +2119,7 @@ constexpr int trace_waves() {
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
 #ifndef RMR_QUEUE_PARTS
-#define RMR_QUEUE_PARTS 8   // work-queue partitions (counters), rmr_internal.h kQueueWords
+#define RMR_QUEUE_PARTS 16   // work-queue partitions (counters; rmr_internal.h kQueueBytes)
 #endif
 #define RMR_QUEUE_STRIDE 32   // 32-bit words between two partition counters (128 B)
 static_assert(RMR_QUEUE_PARTS >= 1 && RMR_QUEUE_PARTS * RMR_QUEUE_STRIDE * 4 <= (int)kQueueBytes, "queue counters");
@@ -2146,11 +2146,12 @@ RMR_D void trace_main(const KParams& P) {
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
     // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
-    // apart): a wave starts on partition blockIdx % parts — the XCD its block was dispatched to, for
-    // the round-robin block dispatch over the 8 XCDs — and moves on to the next partition when its own
-    // is used up. One counter shared by every wave of the chip serialises its atomics: RM2's short
-    // paths fetch ~80 chunks per microsecond, and one counter held its kernel at 3.2 ms against 1.2 ms
-    // with four chunks per atomic (tools/r04_ab2.sh).
+    // apart): a wave starts on partition blockIdx % parts (with 8 or 16 partitions, blocks of one XCD
+    // under the round-robin block dispatch over the 8 XCDs) and moves on to the next partition when
+    // its own is used up. One counter shared by every wave of the chip serialises its atomics: RM2's
+    // short paths fetch ~80 chunks per microsecond, and one counter held its 1080p 16-spp frame at
+    // 3.24 ms against 0.98 / 0.97 ms with 8 / 16 partitions (tools/r04_ab3.sh; Cornell-5, RM3,
+    // multilight, the Mandelbulb 1-2.5% faster with 16 than with one counter).
     const uint32_t n_chunks = (n_units + CHUNK - 1) / CHUNK;
     auto part_begin = [&](uint32_t q) -> uint32_t {   // first unit of partition q (q = parts: the end)
         return (uint32_t)(((uint64_t)n_chunks * q) / (uint32_t)RMR_QUEUE_PARTS) * CHUNK;
