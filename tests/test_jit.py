@@ -123,6 +123,31 @@ def test_jit_samples_bitexact_vs_oracle(renderer, name, path, variant, overrides
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rect,spp", [((0, 0, 8, 8), 1), ((0, 0, 40, 24), 2), ((0, 0, 40, 24), 3),
+                                      ((0, 0, 64, 64), 9)])
+def test_work_queue_partitions_cover_every_unit(renderer, rect, spp):
+    """The trace kernel's work queue in 16 partitions of 128-unit chunks (rmr_trace.h trace_main:
+    a wave starts on partition blockIdx % 16, walks on or scans the counters when its own is used up).
+    Launches of 1, 15, 23 and 288 chunks — fewer, about as many and more chunks than partitions,
+    partial last chunks, the small-launch scan and the walk — against the oracle, every sample."""
+    W, H = 64, 64
+    prm, view = _setup(renderer, os.path.join(SCENES, "cornell5.scene"), "rm1", W, H, {"max_bounces": 2})
+    times = time_schedule(spp, frame=4)
+    renderer.set_jit(1)
+    try:
+        renderer.reset_stats()
+        gpu = renderer.trace_samples(times, rect)
+        st = renderer.stats()
+    finally:
+        renderer.set_jit(2)
+    assert st.jit_launches > 0
+    cpu = oracle.Oracle(_tables(os.path.join(SCENES, "cornell5.scene"), "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
+
+
+@pytest.mark.gpu
 def test_jit_matches_table_kernel_on_large_render(renderer):
     W, H = 256, 192
     _setup(renderer, os.path.join(SCENES, "cornell5.scene"), "rm1", W, H, {"max_bounces": 4})
