@@ -415,10 +415,12 @@ int ensure_jit(rmr_ctx* c) {
     // instructions in round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default
     // +1.2%, tools/env_ab.py shade_t)
     // Kernels with node-program materials (longer shading): 20 (round 4, tools/r04_ab3.sh, 1080p 16
-    // spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24: -6% / +1.4%)
+    // spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24: -6% / +1.4%); the
+    // nearest-primitive cache kernels (their shading batch runs the certified probes): 20 as well
+    // (tools/r04_ab10.sh, csg256 1080p 8 spp: 16.83 -> 16.68 ms; 24: 16.81)
     if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
         k.shade_t = 8;
-    else if (src.find("rmr::JitMats>") != std::string::npos)
+    else if (src.find("rmr::JitMats>") != std::string::npos || k.chunk == 64)
         k.shade_t = 20;
     else
         k.shade_t = 16;
