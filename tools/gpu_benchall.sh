@@ -8,7 +8,7 @@ tail -1 gpurun_out/bench_c2.log | cut -c1-330
 # short frames (C1 0.1 ms, RM2 1 ms, RM3 3 ms) get enough steps for the two overlapping contexts'
 # steady state (3 steps are mostly pipeline fill)
 for c in c1 c3 c5 rm3 rm2; do
-  st=3; [ $c = c1 ] && st=200; [ $c = rm3 ] && st=30; [ $c = rm2 ] && st=60
+  st=3; [ $c = c1 ] && st=200; [ $c = rm3 ] && st=30; [ $c = rm2 ] && st=60; [ $c = c3 ] && st=5
   timeout -k 10 300 python bench.py --config $c --steps $st --warmup 2 > gpurun_out/bench_$c.log 2>&1 || exit $?
   tail -1 gpurun_out/bench_$c.log | cut -c1-330
 done
