@@ -122,3 +122,27 @@ def test_product_refuses_without_gpu_or_fails_loudly():
         pytest.skip("GPU present")
     h = C.c_void_p()
     assert lib().rmr_create(C.byref(h), 0) == -2
+
+
+def test_embedded_kernel_sources_drop_comments_only():
+    """csrc/tools/embed.py ships the device sources inside the library for hipRTC without their
+    comments (which name diagnostic-build switches): string and character literals, preprocessor lines
+    and the line numbering must survive."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "embed_mod", os.path.join(os.path.dirname(__file__), "..", "raymarchrenderer_amd", "csrc", "tools", "embed.py"))
+    src = open(spec.origin).read()
+    ns = {}
+    exec(compile(src.split("\nout, pairs =")[0], spec.origin, "exec"), ns)   # the function, not the script
+    strip = ns["strip_comments"]
+    text = ('#define A 1 // a comment\nint x = 2; /* two\nlines */ int y;\n'
+            'const char* s = "// not a comment /* nor this */";\nchar c = \'"\'; char d = \'\\\'\';  // tail\n'
+            'printf("%d\\n", x); // RMR_JIT_OPTS\n')
+    out = strip(text)
+    assert out.count("\n") == text.count("\n")
+    assert "comment" not in out.replace("not a comment", "")
+    assert "RMR_JIT_OPTS" not in out and "tail" not in out
+    assert '"// not a comment /* nor this */"' in out
+    assert "char c = '\"';" in out and "char d = '\\'';" in out
+    assert "#define A 1" in out and "int y;" in out and 'printf("%d\\n", x);' in out
