@@ -57,11 +57,13 @@ def main(tag, config="c2"):
     gs = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
     big = max(gs(r) for r in kt)
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt if gs(r) == big]
-    if len(durs) != len(kt):
-        out["k_trace_avg_ns_all_launches"] = out["k_trace_avg_ns"]
-        out["k_trace_avg_ns"] = sum(durs) / len(durs)
-        out["k_trace_calls"] = len(durs)
-        out["k_trace_note"] = "production launches only (grid %d); %d smaller launch(es) excluded" % (big, len(kt) - len(durs))
+    # the first production launch is the bench's warm-up step, which its own timing leaves out too
+    warm = 1 if len(durs) > 1 else 0
+    out["k_trace_avg_ns_all_launches"] = out["k_trace_avg_ns"]
+    out["k_trace_avg_ns"] = sum(durs[warm:]) / len(durs[warm:])
+    out["k_trace_calls"] = len(durs) - warm
+    out["k_trace_note"] = ("production launches (grid %d) after the warm-up one; %d smaller launch(es) excluded"
+                           % (big, len(kt) - len(durs)))
     c = {}
     meta = {}
     for d in ("pmcf", "pmcw", "pmcs", "pmcv"):
