@@ -418,9 +418,12 @@ int ensure_jit(rmr_ctx* c) {
     // spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24: -6% / +1.4%); the
     // nearest-primitive cache kernels (their shading batch runs the certified probes): 20 as well
     // (tools/r04_ab10.sh, csg256 1080p 8 spp: 16.83 -> 16.68 ms; 24: 16.81)
+    // The approximate sphere/box kernels with certified probes (Cornell-5) at 7 waves per SIMD: 20 as
+    // well (tools/r04_ab12.sh, 1080p 64 spp: 47.17 -> 46.63 ms; 18: 46.77, 14: 47.92)
     if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
         k.shade_t = 8;
-    else if (src.find("rmr::JitMats>") != std::string::npos || k.chunk == 64)
+    else if (src.find("rmr::JitMats>") != std::string::npos || k.chunk == 64 ||
+             src.find("static constexpr bool kCert = true;") != std::string::npos)
         k.shade_t = 20;
     else
         k.shade_t = 16;
