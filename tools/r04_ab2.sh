@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-4 A/B, second part (diagnostic library; logs in gpurun_out/r04ab_*.log): certified probes of
 # the cache kernels, RM2 wave targets, RM2's light-side shadow bound, C3's RNG state in LDS, C4
-# without its sample-plane stores (timing bound), chunks per work-queue atomic, C2 shading threshold.
+# without its sample-plane stores (timing bound), chunks per work-queue atomic (RMR_SUPER: a diagnostic
+# option removed again once the partitioned queue replaced it), C2 shading threshold.
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 export RMR_LIB=diag
