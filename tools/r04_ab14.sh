@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round-4 A/B, fourteenth part (diagnostic library): the stepped Mandelbulb map with two estimator
 # iterations per pass (an RMR_MB_PASS option, removed again after this measurement: +1.2%)
-# iterations per pass (C3 1080p 128 spp).
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 export RMR_LIB=diag
