@@ -376,7 +376,8 @@ int ensure_jit(rmr_ctx* c) {
     int npc_k = (c->map_np == -2 && c->grid_on) ? 1 : 2;
     if (const char* e = RMR_ENV("RMR_NPC_KSEL")) npc_k = std::atoi(e) == 1 ? 1 : 2;   // (experiments)
     const bool npc_spheres = c->map_np == -2 && c->grid_on && c->grid_small_spheres;
-    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k, npc_spheres);
+    rmr::JitFacts facts;
+    const std::string src = rmr::jit_source(c->scene, c->has_prog, true, c->cull, &c->jit_live, npc_k, npc_spheres, &facts);
     std::vector<char> code;
     std::string key, log;
     std::vector<std::string> opts;
@@ -406,27 +407,18 @@ int ensure_jit(rmr_ctx* c) {
         return fail(c, RMR_E_HIP, "rmr_jit_trace missing from the specialised code object (key " + key + ")");
     }
     k.block = 256;
-    k.chunk = src.find("TableMap<-3>") != std::string::npos ? 64 : 128;
+    k.chunk = facts.chunk();
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
-    // general maps without material programs, whose map() dwarfs the shading (the Mandelbulb): 8
-    // (C3 +2-3%); otherwise 16 (RM1 inline sphere/box maps: 20 until the map() loop lost ~12% of its
-    // instructions in round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default
-    // +1.2%, tools/env_ab.py shade_t)
-    // Kernels with node-program materials (longer shading): 20 (round 4, tools/r04_ab3.sh, 1080p 16
-    // spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24: -6% / +1.4%); the
-    // nearest-primitive cache kernels (their shading batch runs the certified probes): 20 as well
-    // (tools/r04_ab10.sh, csg256 1080p 8 spp: 16.83 -> 16.68 ms; 24: 16.81)
-    // The approximate sphere/box kernels with certified probes (Cornell-5) at 7 waves per SIMD: 20 as
-    // well (tools/r04_ab12.sh, 1080p 64 spp: 47.17 -> 46.63 ms; 18: 46.77, 14: 47.92)
-    if (src.find("rmr::trace_waves<1, true, false>") != std::string::npos)
-        k.shade_t = 8;
-    else if (src.find("rmr::JitMats>") != std::string::npos || k.chunk == 64 ||
-             src.find("static constexpr bool kCert = true;") != std::string::npos)
-        k.shade_t = 20;
-    else
-        k.shade_t = 16;
+    // shading batch per kernel class (rmr_jit.hpp JitFacts::shade_t). Measured: the Mandelbulb 8 (C3
+    // +2-3%); RM1 inline sphere/box maps 16 (20 until the map() loop lost ~12% of its instructions in
+    // round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default +1.2%); node-program
+    // materials 20 (round 4, 1080p 16 spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24:
+    // -6% / +1.4%); the cache kernels 20 (csg256 1080p 8 spp: 16.83 -> 16.68 ms; 24: 16.81); the
+    // certified sphere/box kernels at 7 waves 20 (Cornell-5 1080p 64 spp: 47.17 -> 46.63 ms; 18: 46.77,
+    // 14: 47.92)
+    k.shade_t = facts.shade_t();
     c->jit_loaded.push_back(k);
     c->jit = k;
     c->jit_ready = true;

@@ -42,6 +42,23 @@ struct JitKernel {
                                 // RMR_CHUNK; the nearest-primitive cache kernels: RMR_CHUNK_CACHE)
 };
 
+// What jit_source decided about the kernel class (the launch settings follow from these, not from
+// the text of the source): the nearest-primitive cache map (TableMap<-3>: 64-unit chunks), a general
+// map (Mandelbulb / node-program objects), node-program materials, certified getNormal probes.
+struct JitFacts {
+    int variant = 0;
+    bool cache = false, general = false, prog = false, cert = false;
+    int chunk() const { return cache ? 64 : 128; }   // rmr_trace.h RMR_CHUNK_CACHE / RMR_CHUNK
+    // default shading batch: general maps without material programs, whose map() dwarfs the shading
+    // (the Mandelbulb): 8 (C3 +2-3%); node-program materials, the cache kernels and the certified
+    // sphere/box kernels (their batches run the certified probes): 20; otherwise 16 (rmr_api.cpp)
+    int shade_t() const {
+        if (variant == RMR_VARIANT_RM1 && general && !prog) return 8;
+        if (prog || cache || cert) return 20;
+        return 16;
+    }
+};
+
 // HIP source of the specialised trace kernel for `s` (entry point "rmr_jit_trace"). bake: the
 // primitives' numbers are literals (fastest: +6-12% over loading them); otherwise only the scene's
 // structure is compiled and the numbers are scalar loads, so a scene that only moves (an animation)
@@ -52,8 +69,10 @@ struct JitKernel {
 // npc_k: primitives per lane in the nearest-primitive cache (RMR_NPC_K: 1 or 2) of BVH scenes.
 // npc_spheres: every primitive the candidate grid lists is a sphere (RMR_NPC_SPHERES: the full
 // map's candidates take the sphere distance, the same value as the general form for a sphere).
+// facts (optional): the kernel class, for the launch settings.
 std::string jit_source(const CompiledScene& s, bool prog, bool bake = true, int cull = 7,
-                       const std::vector<char>* live = nullptr, int npc_k = 2, bool npc_spheres = false);
+                       const std::vector<char>* live = nullptr, int npc_k = 2, bool npc_spheres = false,
+                       JitFacts* facts = nullptr);
 // Compile `src` for gfx950 (no GPU needed). Code-object cache: in-process, then the directory
 // $RMR_JIT_CACHE (default $HOME/.cache/rmr-jit). Returns false with the compiler log in `log`.
 // opts: further compiler options, part of the key (the instrumented build of rmr_set_instrument:

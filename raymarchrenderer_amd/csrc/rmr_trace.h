@@ -1892,7 +1892,7 @@ RMR_D void shade(const KParams& P, Lane& L) {
         const bool want = (L.phase == PH_HIT);
         const int id = want ? (int)L.mid : -1;
         int kind = MAT_NONE;
-        DMat dm;
+        DMat dm{};
         if (want && id >= 0 && id < P.n_mats) {
             dm = P.dmats[id];
             kind = dm.kind;
@@ -2071,6 +2071,34 @@ RMR_D uint32_t lane_now() {
     return v;
 }
 
+// a defined value the compiler cannot see (no constant to propagate into the loop PHIs): trace_main's
+// lane at kernel entry; the inline asm emits no instruction
+RMR_D float opq() {
+    float v;
+    __asm__ volatile("; lane init %0" : "=v"(v));
+    return v;
+}
+RMR_D V3 opq3() { return v3(opq(), opq(), opq()); }
+RMR_D void lane_define(Lane& L) {
+    L.unit = __float_as_uint(opq());
+    L.gxt = opq(); L.gyt = opq(); L.rc = opq();
+    L.o = opq3(); L.d = opq3();
+    L.t = opq();
+    L.ctr = __float_as_int(opq());
+    L.hit = opq3();
+    L.mid = opq();
+    L.nrm = opq3();
+    L.color = opq3();
+    L.chan = __float_as_int(opq()); L.bounces = __float_as_int(opq());
+    L.inside = false;
+    L.time = opq();
+    L.fin = opq3();
+    L.wl = __float_as_uint(opq());
+    L.power = opq();
+    L.cw = __float_as_int(opq()); L.cw2 = __float_as_int(opq());
+    L.cs = opq(); L.cta = opq(); L.texit = opq();
+    L.e = opq3();
+}
 RMR_D bool is_active(int ph) { return (uint32_t)ph <= (uint32_t)PH_SHADOW; }   // PH_DONE (-1) is not
 RMR_D bool is_shade(int ph) { return ph >= PH_HIT; }   // (PH_DONE, -1, is not)
 
@@ -2094,11 +2122,11 @@ RMR_D bool is_shade(int ph) { return ph >= PH_HIT; }   // (PH_DONE, -1, is not)
 #ifndef RMR_CACHE_WAVES
 #define RMR_CACHE_WAVES 6
 #endif
-// waves/SIMD target of the kernels with node-program materials (1 = none: the allocator's choice, 4
-// waves at ~110-120 VGPRs). Forcing 6-7 was 5-9% faster on default.scene / multilight, but the 7-wave
-// build of glass_test.scene (26 VGPRs and 40 SGPRs spilled) rendered wrong samples (sky pixels at
-// 0.8x, against the oracle), so the setting stays with the allocator (tools/env_ab.py RMR_JIT_OPTS
-// -DRMR_PROG_WAVES=N for experiments only)
+// waves/SIMD target of the kernels with node-program materials (1 = none: the allocator's choice, 4-6
+// waves at 79-120 VGPRs; the hipRTC kernels set 6, rmr_jit.cpp). Until round 5 the 6 / 7-wave builds of
+// glass_test.scene rendered wrong samples: `Lane L;` left lane fields undefined, the IR carried undef
+// PHIs into the persistent loop, and the allocator's live-range splitting dropped the prologue's
+// throughput on some refill paths (trace_main now defines every field: lane_define)
 #ifndef RMR_PROG_WAVES
 #define RMR_PROG_WAVES 1
 #endif
@@ -2137,10 +2165,17 @@ RMR_D void trace_main(const KParams& P) {
     // certified hits (march_update: ctr = -1) get getNormal's probes in the shading batch from one
     // primitive: the approximate sphere/box maps' certificate (MAP::kCert), the one-primitive cache's
     constexpr bool CERT = HO && (MAP::kCert || (MAP::kCache && RMR_NPC_K == 1 && RMR_CACHE_CERT));
+    // Every lane field defined before the persistent loop. With `Lane L;` alone the optimised IR had
+    // `phi [undef, %entry]` at the loop header for each field, and the allocator's live-range
+    // splitting was then free to lose a lane's value on refill paths (the round-4 6 / 7-wave glass_test
+    // miscompute; tests/test_kernel_ir.py, test_gpu_prog_waves.py). Opaque values (lane_define), not
+    // `Lane L{}`: zeros give the optimiser constants to propagate through the loop PHIs, which cost
+    // the Cornell-5 kernel 20 spilled VGPRs (C2 +0.8%, C3 +1.0%, same process)
     Lane L;
+    lane_define(L);
     L.phase = PH_IDLE;
     init_probe(L);
-    MBStep mbs;   // stepped map() state (MAP::kStepped); i < 0: no map() in progress
+    MBStep mbs{};   // stepped map() state (MAP::kStepped); i < 0: no map() in progress
     mbs.i = -1;
     mbs.fin = false;
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
@@ -2402,8 +2437,8 @@ RMR_D void trace_main(const KParams& P) {
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
                     RMR_STAMP(f0);
                     if (act1 && !ok) {
-                        int kw, kw2;
-                        float s2;
+                        int kw = -1, kw2 = 0;   // (written by every path of MAP::full: defined for the compiler too)
+                        float s2 = -__builtin_inff();
                         // seeded with the cached primitive only at a finite point: prim_dist's box form
                         // of a sphere drops a NaN coordinate (fmaxf / fminf) where sd_sphere keeps it
                         m = MAP::full(P, p, kw, kw2, s2, (pfin && F == F) ? L.cw : -1, jw, F, mid, RMR_DTAB);
