@@ -154,10 +154,14 @@ def cpu_threads():
 
 
 def cpu_baseline(cfg, spp, seconds, threads, repeats=3):
-    """CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload: 40 rows
-    spread over the frame, samples 0.. of the same schedule. `repeats` timed runs of ~seconds/repeats
-    each after one untimed warm-up row pass; the median is reported."""
+    """CPU leg on a bounded sample of the same workload: 40 rows spread over the frame, samples 0.. of
+    the same schedule. `repeats` timed runs of ~seconds/repeats each after an untimed warm-up; the
+    median is reported. RM1 configs run the vectorised port (oracle/rmr_cpu_wave.c:
+    the oracle's path 8 lanes at a time on AVX2, as the reference's llvmpipe JIT runs 8 invocations per
+    vector; bitwise the scalar oracle, tests/test_cpu_wave.py), with the scalar oracle (the checker)
+    timed beside it; RM2 / RM3 configs run the scalar oracle."""
     import statistics
+    import numpy as np
     from oracle import camera, oracle
     from raymarchrenderer_amd import abi, time_schedule
     W, H = cfg["W"], cfg["H"]
@@ -173,34 +177,63 @@ def cpu_baseline(cfg, spp, seconds, threads, repeats=3):
     ns = min(spp, 4)
     units = [(rows[i], s) for i in order for s in range(ns)]
     times = time_schedule(spp)
-    # untimed warm-up (~1/8 of the budget): the OpenMP pool and the cores' clocks settle (measured: the
-    # first second of RM3 rows ran up to 10x slower than the same rows afterwards)
-    t0, i = time.perf_counter(), 0
-    while time.perf_counter() - t0 < seconds / 8:
-        y, s = units[i % len(units)]
-        o.render(times[s:s + 1], rect=(0, y, W, y + 1), first_sample=s, nthreads=threads)
-        i += 1
-    rates, total = [], 0
-    for _ in range(repeats):
-        done = 0
-        i = 0
-        t0 = time.perf_counter()
-        while True:
+    wave = o.render_wave(times[0:1], rect=(0, 0, 1, 1), nthreads=1) is not None
+
+    acc = np.zeros((H, W, 4), np.float32)   # one accumulator for every call (a fresh 33 MB array per
+                                            # row call measured ~4 ms of the call's time)
+
+    def timed(render, secs, reps, units, per_call):
+        # untimed warm-up (~1/8 of the budget): the OpenMP pool and the cores' clocks settle (measured:
+        # the first second of RM3 rows ran up to 10x slower than the same rows afterwards)
+        t0, i = time.perf_counter(), 0
+        while time.perf_counter() - t0 < secs / 8:
             y, s = units[i % len(units)]
-            o.render(times[s:s + 1], rect=(0, y, W, y + 1), first_sample=s, nthreads=threads)
-            done += W
+            render(times[s:s + 1], rect=None if y is None else (0, y, W, y + 1), first_sample=s, accum=acc,
+                   nthreads=threads)
             i += 1
-            if time.perf_counter() - t0 >= seconds / repeats:
-                break
-        rates.append(done / (time.perf_counter() - t0) / 1e6)
-        total += done
+        rates, total = [], 0
+        for _ in range(reps):
+            done, i = 0, 0
+            t0 = time.perf_counter()
+            while True:
+                y, s = units[i % len(units)]
+                render(times[s:s + 1], rect=None if y is None else (0, y, W, y + 1), first_sample=s, accum=acc,
+                       nthreads=threads)
+                done += per_call
+                i += 1
+                if time.perf_counter() - t0 >= secs / reps:
+                    break
+            rates.append(done / (time.perf_counter() - t0) / 1e6)
+            total += done
+        return rates, total
+
+    if wave:
+        # the vectorised port takes one sample of every sampled row per call (one batch shared by the
+        # threads: a call per row would drain the lanes 40 times as often); the same samples
+        def render(t, rect, first_sample, accum, nthreads):
+            return o.render_wave_rows(t, rows, first_sample=first_sample, accum=accum, nthreads=nthreads)
+        vunits = [(None, s) for s in range(ns)]
+        rates, total = timed(render, seconds, repeats, vunits, len(rows) * W)
+    else:
+        rates, total = timed(o.render, seconds, repeats, units, W)
+    impl = ("AVX2 8-lane wavefront port (oracle/rmr_cpu_wave.c), bitwise the scalar oracle" if wave
+            else "scalar C restatement (oracle/rmr_oracle.c)")
     out = {"value": statistics.median(rates), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "per_core": round(statistics.median(rates) / threads, 4), "implementation": impl,
            "repeats_msamples_per_s": [round(x, 4) for x in rates],
            "sample": "median of %d timed runs (%d samples in all) of the same work: rows y%%%d==0 of the %dx%d "
-                     "frame (bit-reversed order) x the schedule's first %d samples, %d-thread OpenMP C restatement (oracle/rmr_oracle.c); %d threads = every CPU "
-                     "of this process's affinity set, capped by OMP_NUM_THREADS (the host-CPU share of one GPU "
-                     "on the GPU box)" % (repeats, total, stride, W, H, ns, threads, threads),
+                     "frame x the schedule's first %d samples (%s), %d-thread OpenMP %s; %d threads "
+                     "= every CPU of this process's affinity set, capped by OMP_NUM_THREADS (the host-CPU share of "
+                     "one GPU on the GPU box)" % (repeats, total, stride, W, H, ns,
+                                                  "one call per sample over all the rows" if wave else
+                                                  "one call per row and sample, rows in bit-reversed order",
+                                                  threads, impl, threads),
            "host_cpus_visible": os.cpu_count()}
+    if wave:
+        # the scalar oracle (the checker) on the same work, one short run, for comparison
+        srates, stotal = timed(o.render, max(2.0, seconds / 4), 1, units, W)
+        out["scalar_port"] = {"value": round(srates[0], 4), "per_core": round(srates[0] / threads, 4),
+                              "samples": stotal, "implementation": "scalar C restatement (oracle/rmr_oracle.c)"}
     ref = LLVMPIPE_PER_VCPU.get(cfg_name_of(cfg))
     if ref:
         # the reference's own path (RayMarch.glsl on Mesa llvmpipe) cannot run on the GPU box (no

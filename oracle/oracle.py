@@ -12,7 +12,9 @@ from raymarchrenderer_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RMR_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")   # (sanitizer test)
+WAVE_LIB_PATH = os.path.join(HERE, "libcpu_wave.so")
 _lib = None
+_wave = None
 
 
 def build():
@@ -26,6 +28,24 @@ def lib():
             build()
         _lib = load(LIB_PATH)
     return _lib
+
+
+def wave_lib():
+    """libcpu_wave.so (oracle/rmr_cpu_wave.c): bench.py's CPU baseline for RM1 scenes, the oracle's
+    path 8 lanes at a time on AVX2, bitwise the oracle's results."""
+    global _wave
+    if _wave is None:
+        if not os.path.exists(WAVE_LIB_PATH):
+            build()
+        _wave = load(WAVE_LIB_PATH)
+        fp = C.POINTER(C.c_float)
+        _wave.oracle_render_wave.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                             C.c_uint32, fp, C.c_int, C.POINTER(C.c_uint64)]
+        _wave.oracle_render_wave.restype = C.c_int
+        _wave.oracle_render_wave_rows.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32),
+                                                  C.c_int, C.c_uint32, C.c_uint32, fp, C.c_int, C.POINTER(C.c_uint64)]
+        _wave.oracle_render_wave_rows.restype = C.c_int
+    return _wave
 
 
 def literal_lib():
@@ -106,6 +126,40 @@ class Oracle:
         n = C.c_uint64(0)
         lib().oracle_render(C.byref(self.job), _fp(times), x0, y0, x1, y1, first_sample, len(times),
                             _fp(accum), nthreads, C.byref(n))
+        self.map_evals += n.value
+        return accum
+
+    def render_wave(self, times, rect=None, first_sample=0, accum=None, nthreads=0):
+        """render() through the 8-lane AVX2 wavefront (oracle/rmr_cpu_wave.c), RM1 scenes only (None
+        otherwise): the same accumulator bit for bit, several times faster per core."""
+        times = np.ascontiguousarray(times, np.float32)
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
+        if accum is None:
+            accum = np.zeros((self.H, self.W, 4), np.float32)
+        n = C.c_uint64(0)
+        rc = wave_lib().oracle_render_wave(C.byref(self.job), _fp(times), x0, y0, x1, y1, first_sample, len(times),
+                                           _fp(accum), nthreads, C.byref(n))
+        if rc != 0:
+            return None
+        self.map_evals += n.value
+        return accum
+
+    def render_wave_rows(self, times, rows, first_sample=0, accum=None, nthreads=0):
+        """render_wave() of whole rows `rows` (distinct row indices) in one call: one batch of
+        len(rows) x W x len(times) samples shared by every thread (fewer lane drains than a call per
+        row). None for RM2 / RM3 scenes."""
+        times = np.ascontiguousarray(times, np.float32)
+        r = np.ascontiguousarray(rows, np.int32)
+        if accum is None:
+            accum = np.zeros((self.H, self.W, 4), np.float32)
+        n = C.c_uint64(0)
+        rc = wave_lib().oracle_render_wave_rows(C.byref(self.job), _fp(times), 0, self.W, 0,
+                                                r.ctypes.data_as(C.POINTER(C.c_int32)), len(r), first_sample,
+                                                len(times), _fp(accum), nthreads, C.byref(n))
+        if rc == -1:
+            return None
+        if rc != 0:
+            raise ValueError("oracle_render_wave_rows: row out of range")
         self.map_evals += n.value
         return accum
 

@@ -41,12 +41,16 @@ def build():
 
 
 def lib(diag=None):
-    """The ctypes handle of librmr.so, or of librmr_diag.so with diag=True. diag=None: the release
+    """The ctypes handle of librmr.so, or of librmr_diag.so with diag=True, or of the library file
+    diag names (a str: another build of the same ABI, for same-process A/B runs). diag=None: the release
     library unless the environment selects the diagnostic one with RMR_LIB=diag (tools/ scripts;
     the selection is made here, in Python: the release library itself reads no such switch)."""
     if diag is None:
         diag = os.environ.get("RMR_LIB", "") == "diag"
-    path = LIB_DIAG_PATH if diag else LIB_PATH
+    if isinstance(diag, str):   # a library file (tools/abrun.py: another build of the same ABI)
+        path = os.path.abspath(diag)
+    else:
+        path = LIB_DIAG_PATH if diag else LIB_PATH
     if path in _libs:
         return _libs[path]
     if not os.path.exists(path):
@@ -116,6 +120,8 @@ def lib(diag=None):
                                          C.POINTER(C.c_uint16), C.c_size_t]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(L, name):   # (an older build given by path may lack a newer entry point)
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

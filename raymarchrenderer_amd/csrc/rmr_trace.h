@@ -734,6 +734,14 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 #ifndef RMR_NPC_LDS_MAX
 #define RMR_NPC_LDS_MAX 256
 #endif
+// 1: the scene has <= RMR_NPC_LDS_MAX primitives, the table is always in LDS (the hipRTC kernels know
+// it: rmr_jit.cpp); 0: always global; -1: decided per launch (the ahead-of-time kernels). A per-launch
+// choice leaves a select between an LDS and a global pointer, which the compiler can only serve with
+// generic flat_load instructions: on C4 that was 2e10 flat loads per frame, each counted against both
+// vmcnt and lgkmcnt (profiles/r05_attr_c4.json), instead of ds_read_b128
+#ifndef RMR_NPC_DP_LDS
+#define RMR_NPC_DP_LDS -1
+#endif
 RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j) {
     const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type|index<<8 mat_id
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
@@ -2245,7 +2253,7 @@ RMR_D void trace_main(const KParams& P) {
 #endif
     constexpr bool kSeeds = MAP::kStepped && PERSIST && RMR_SEED_LDS;
     __shared__ float s_rng[kSeeds ? 3 : 1][4][kSeeds ? 64 : 1];
-    const bool dp_lds = MAP::kCache && P.n_prims <= RMR_NPC_LDS_MAX;
+    const bool dp_lds = MAP::kCache && (RMR_NPC_DP_LDS >= 0 ? RMR_NPC_DP_LDS == 1 : P.n_prims <= RMR_NPC_LDS_MAX);
     if (dp_lds) {
         for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
         __syncthreads();

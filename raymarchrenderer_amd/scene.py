@@ -20,18 +20,20 @@ class CompiledScene:
             text = scene or ""
         b = text.encode()
         self._h = C.c_void_p()
+        # the library is chosen once per handle: free (and view) go to the library that compiled it
+        self._L = lib()
         err = C.create_string_buffer(512)
-        rc = lib().rmr_scene_compile(variant, b, len(b), C.byref(self._h), err, len(err))
+        rc = self._L.rmr_scene_compile(variant, b, len(b), C.byref(self._h), err, len(err))
         if rc != abi.RMR_OK:
             raise RMRError(rc, err.value.decode(errors="replace"))
         self.variant = variant
         self.view = abi.Scene()
-        lib().rmr_scene_view(self._h, C.byref(self.view))
+        self._L.rmr_scene_view(self._h, C.byref(self.view))
 
     def __del__(self):
         try:
             if self._h:
-                lib().rmr_scene_free(self._h)
+                self._L.rmr_scene_free(self._h)
         except Exception:
             pass
 

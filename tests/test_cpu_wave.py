@@ -1,0 +1,81 @@
+"""bench.py's vectorised CPU baseline (oracle/rmr_cpu_wave.c: the oracle's RM1 path 8 lanes at a time
+on AVX2) is bitwise the scalar oracle (oracle/rmr_oracle.c, the checker) on sampled rows of every RM1
+scene family, the running mean over several samples included, and declines RM2 / RM3 scenes."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import camera, oracle, scene_compile
+from oracle.envmap import synthetic_env
+from raymarchrenderer_amd import abi, time_schedule
+
+from .conftest import GOLDEN, SCENES
+
+CASES = [   # name, scene, param overrides, W, H, rows
+    ("cornell5", os.path.join(SCENES, "cornell5.scene"), {"max_bounces": 4}, 1920, 1080, [0, 540, 1079]),
+    ("sphere1", os.path.join(SCENES, "sphere1.scene"), {"max_bounces": 1}, 256, 256, [0, 128, 200]),
+    ("default", os.path.join(GOLDEN, "scenes", "default.scene"), {}, 320, 180, [60, 90, 170]),
+    ("glass", os.path.join(GOLDEN, "scenes", "glass_test.scene"), {}, 320, 180, [40, 100, 150]),
+    ("multilight", os.path.join(GOLDEN, "scenes", "multilight.scene"), {}, 320, 180, [30, 95, 160]),
+    ("glass_sepch", os.path.join(GOLDEN, "scenes", "glass_test.scene"), {"separate_channels": 1}, 160, 90, [45, 60]),
+    ("glass_step17", os.path.join(GOLDEN, "scenes", "glass_test.scene"), {"step_multiply": 1.7, "max_dist": 12.0}, 160, 90, [45, 70]),
+    ("cornell5_steps8", os.path.join(SCENES, "cornell5.scene"), {"max_bounces": 4, "max_steps": 8}, 320, 180, [90]),
+    ("cornell5_b0", os.path.join(SCENES, "cornell5.scene"), {"max_bounces": 0}, 64, 36, [10]),
+    ("sphere1_env", os.path.join(SCENES, "sphere1.scene"), {"max_bounces": 4, "use_env_tex": 1}, 128, 128, [30, 64]),
+    ("mandelbulb", os.path.join(SCENES, "mandelbulb.scene"), {"max_bounces": 2}, 192, 108, [54]),
+    ("csg_nodes", os.path.join(SCENES, "csg_nodes.scene"), {"max_bounces": 4}, 192, 108, [50]),
+    ("csg64", os.path.join(SCENES, "csg64.scene"), {"max_bounces": 4}, 192, 108, [60]),
+]
+
+
+@pytest.mark.parametrize("name,path,over,W,H,rows", CASES, ids=[c[0] for c in CASES])
+def test_wave_baseline_bitwise_equal_to_oracle(name, path, over, W, H, rows):
+    prm = abi.default_params(**over)
+    env = synthetic_env() if prm.use_env_tex else None
+    o = oracle.Oracle(scene_compile.load_scene_file(path, "rm1"), prm, camera.default_view(W, H), W, H, env=env)
+    times = time_schedule(3, frame=1)
+    for y in rows:
+        rect = (3, y, W - 2, y + 1)
+        a = o.render(times, rect=rect, first_sample=5, nthreads=2)
+        b = o.render_wave(times, rect=rect, first_sample=5, nthreads=2)
+        assert b is not None
+        same = a.view(np.uint32) == b.view(np.uint32)
+        assert same.all(), "%s row %d: %d of %d words differ" % (name, y, (~same).sum(), same.size)
+
+
+def test_wave_rows_equal_to_per_row_oracle_calls():
+    """The bench's call shape: every sampled row of the frame in one call, one sample per call."""
+    W, H = 480, 270
+    prm = abi.default_params(max_bounces=4)
+    o = oracle.Oracle(scene_compile.load_scene_file(os.path.join(SCENES, "cornell5.scene"), "rm1"), prm,
+                      camera.default_view(W, H), W, H)
+    rows = [0, 131, 27, 269, 54]
+    times = time_schedule(3)
+    a = np.zeros((H, W, 4), np.float32)
+    b = np.zeros((H, W, 4), np.float32)
+    for s in range(3):
+        for y in rows:
+            o.render(times[s:s + 1], rect=(0, y, W, y + 1), first_sample=s, accum=a, nthreads=2)
+        o.render_wave_rows(times[s:s + 1], rows, first_sample=s, accum=b, nthreads=3)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    with pytest.raises(ValueError):
+        o.render_wave_rows(times[:1], [H], accum=b)
+
+
+def test_wave_baseline_counts_the_same_map_calls():
+    W, H = 320, 180
+    prm = abi.default_params(max_bounces=4)
+    tabs = scene_compile.load_scene_file(os.path.join(SCENES, "cornell5.scene"), "rm1")
+    a = oracle.Oracle(tabs, prm, camera.default_view(W, H), W, H)
+    b = oracle.Oracle(tabs, prm, camera.default_view(W, H), W, H)
+    a.render(time_schedule(2), rect=(0, 80, W, 84))
+    b.render_wave(time_schedule(2), rect=(0, 80, W, 84))
+    assert a.map_evals == b.map_evals > 0
+
+
+@pytest.mark.parametrize("variant,path", [("rm2", os.path.join(GOLDEN, "scenes", "simple.scene")), ("rm3", None)])
+def test_wave_baseline_declines_rm2_rm3(variant, path):
+    tabs = scene_compile.compile_scene({}, variant) if path is None else scene_compile.load_scene_file(path, variant)
+    o = oracle.Oracle(tabs, abi.default_params(), camera.default_view(64, 36), 64, 36)
+    assert o.render_wave(time_schedule(1), rect=(0, 0, 64, 1)) is None

@@ -98,9 +98,9 @@ def test_display_rejects_wrong_screen_buffers():
         with pytest.raises(ValueError):
             r.display((8.0, 8.0), 1.0, (0, 0), (16, 16), screen=np.zeros((16, 16, 3), np.uint8))
         buf = np.zeros((16, 16, 4), np.uint8)
-        rc = lib().rmr_display(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, buf.ctypes.data, buf.nbytes - 1)
+        rc = r.lib.rmr_display(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, buf.ctypes.data, buf.nbytes - 1)
         assert rc == RMR_E_INVALID
-        rc = lib().rmr_display_device(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, C.c_void_p(1), 16 * 16 * 4 - 4)
+        rc = r.lib.rmr_display_device(r.ctx, 8.0, 8.0, 1.0, 0.0, 0.0, 16.0, 16.0, 16, 16, C.c_void_p(1), 16 * 16 * 4 - 4)
         assert rc == RMR_E_INVALID
         with pytest.raises(RMRError):
             r.display_device((8.0, 8.0), 1.0, (0, 0), (16, 16), 1, 16, 16, nbytes=100)

@@ -12,7 +12,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
-from raymarchrenderer_amd._lib import lib  # noqa: E402
 
 G = os.path.join(ROOT, "tests", "golden", "scenes")
 r = Renderer(0, 1920, 1080)
@@ -25,8 +24,7 @@ for name, path, b in [("cornell5", os.path.join(ROOT, "scenes", "cornell5.scene"
     r.reset_stats()
     r.render_spp(time_schedule(4))
     st = r.stats()
-    raw = (C.c_uint64 * 16)()
-    lib().rmr_get_counters(r._ctx, raw)
+    raw = r.counters()
     out = [raw[4], raw[5]]
     cls = {"nan_point": raw[6], "exact_tie": raw[7], "near_surface": raw[9], "l2_tiny": raw[10]}
     f = lambda v: float(np.array([v & 0xffffffff], np.uint32).view(np.float32)[0])

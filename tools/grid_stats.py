@@ -15,7 +15,6 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 os.environ["RMR_JIT_OPTS"] = (os.environ.get("RMR_JIT_OPTS", "") + " -DRMR_GRID_STATS").strip()
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
-from raymarchrenderer_amd._lib import lib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=4)
@@ -29,8 +28,7 @@ r.reload()
 r.reset_stats()
 r.render_spp(time_schedule(a.spp))
 st = r.stats()
-c = (C.c_uint64 * 16)()
-lib().rmr_get_counters(r._ctx, c)
+c = r.counters()
 nb = max(1, c[4])
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("RMR_")}, "trace_ms": round(st.trace_ms, 2),
                   "map_iters": st.map_iters, "full_batches": c[3], "grid_batches": c[4],

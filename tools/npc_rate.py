@@ -9,7 +9,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
-from raymarchrenderer_amd._lib import lib  # noqa: E402
 
 r = Renderer(0, 1920, 1080)
 r.set_jit(1)
@@ -20,8 +19,7 @@ for rnd in range(2):
     r.reset_stats()
     r.render_spp(time_schedule(4))
     st = r.stats()
-raw = (C.c_uint64 * 16)()
-lib().rmr_get_counters(r._ctx, raw)
+raw = r.counters()
 print(json.dumps({"full_threshold": os.environ.get("RMR_FULL_T", "default"), "trace_ms": round(st.trace_ms, 2),
                   "map_evals": st.map_evals, "map_iters": st.map_iters, "full_batches": raw[3],
                   "lane_util": round(st.map_evals / (64.0 * st.map_iters), 4),

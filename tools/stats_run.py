@@ -11,7 +11,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("RMR_LIB", "diag")   # tools run against the diagnostic build (env switches)
 from raymarchrenderer_amd import Renderer, abi, time_schedule  # noqa: E402
-from raymarchrenderer_amd._lib import lib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=16)
@@ -31,8 +30,7 @@ r.render_spp(time_schedule(a.spp))   # warm-up (JIT compile)
 r.reset_stats()
 r.render_spp(time_schedule(a.spp))
 st = r.stats()
-raw = (C.c_uint64 * 16)()
-lib().rmr_get_counters(r._ctx, raw)
+raw = r.counters()
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("RMR_")}, "trace_ms": round(st.trace_ms, 3),
                   "map_evals": st.map_evals, "map_iters": st.map_iters, "shade_batches": st.shade_batches,
                   "lanes_shaded": raw[8], "lanes_per_batch": round(raw[8] / max(1, st.shade_batches), 2),

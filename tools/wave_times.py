@@ -33,8 +33,7 @@ for s in [int(x) for x in a.spp.split(",")]:
     r.reset_stats()
     r.render_spp(time_schedule(s))
     r.sync()
-    c = (C.c_uint64 * 16)()
-    lib().rmr_get_counters(r.ctx, c)
+    c = r.counters()
     st = r.stats()
     t0 = M ^ c[9]
     us = lambda t: round((t - t0) / 100.0, 1)   # 100 MHz ticks -> us after the first wave's start
