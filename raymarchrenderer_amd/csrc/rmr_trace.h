@@ -2506,6 +2506,27 @@ RMR_D void trace_main(const KParams& P) {
                 const uint64_t fm = __ballot(is_active(L.phase) && mbs.fin);
                 const uint64_t rm = __ballot(is_active(L.phase) && !mbs.fin);
                 if (fm && (!rm || __popcll(fm) >= RMR_MB_FIN)) {
+#ifdef RMR_MB_STATS   // diagnostics: estimator iterations per finished map, march steps vs normal probes
+                    {
+                        const bool fin_l = is_active(L.phase) && mbs.fin;
+                        const bool nrm_l = L.phase == PH_NORMAL;
+                        uint32_t it_m = (fin_l && !nrm_l) ? (uint32_t)mbs.i : 0u, it_n = (fin_l && nrm_l) ? (uint32_t)mbs.i : 0u;
+                        for (int o = 32; o > 0; o >>= 1) {
+                            it_m += (uint32_t)__shfl_xor((int)it_m, o);
+                            it_n += (uint32_t)__shfl_xor((int)it_n, o);
+                        }
+                        const uint64_t bm_ = __ballot(fin_l && !nrm_l), bn_ = __ballot(fin_l && nrm_l);
+                        if (lane_now() == 0) {
+                            atomicAdd(P.counters + 9, (unsigned long long)__popcll(bm_));
+                            atomicAdd(P.counters + 10, (unsigned long long)it_m);
+                            atomicAdd(P.counters + 12, (unsigned long long)__popcll(bn_));
+                            atomicAdd(P.counters + 13, (unsigned long long)it_n);
+                            atomicAdd(P.counters + 11, (unsigned long long)liters);   // passes up to this batch
+                            atomicAdd(P.counters + 15, 1ull);                         // finishing batches
+                        }
+                        liters = 0;
+                    }
+#endif
                     if (is_active(L.phase) && mbs.fin) {
                         if constexpr (!MAP::kCounts)
                             RMR_COUNT(P.counters, active_lanes(), (uint64_t)P.flops_static, (uint64_t)P.transc_static);

@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--W", type=int, default=0)
     ap.add_argument("--H", type=int, default=0)
+    ap.add_argument("--raw", action="store_true", help="also print the 16 raw kernel counters (diagnostic builds)")
     a = ap.parse_args()
     vs = [parse_variant(t) for t in a.variants]
     keys = sorted({k for v in vs for k in v["env"]})
@@ -132,6 +133,8 @@ def main():
                 "lanes_per_batch": round(cnt[i][8] / max(1, st[i].shade_batches), 2),
                 "bitwise_equal_to_first": bool(np.array_equal(img[i].view(np.uint32), img[0].view(np.uint32))),
             }
+            if a.raw:
+                out[v["label"]]["raw"] = cnt[i]
             if "-DRMR_PROFILE" in v["env"].get("RMR_JIT_OPTS", ""):
                 # section cycles of the profiling build (rmr_trace.h RMR_PROFILE: counters 4-7, 9),
                 # as fractions of the waves' cycles (the s_memtime stamps themselves cost ~10%)
