@@ -146,3 +146,11 @@ def test_embedded_kernel_sources_drop_comments_only():
     assert '"// not a comment /* nor this */"' in out
     assert "char c = '\"';" in out and "char d = '\\'';" in out
     assert "#define A 1" in out and "int y;" in out and 'printf("%d\\n", x);' in out
+    # a block comment is one space (`int/**/x` stays two tokens), and a multi-line one inside a macro
+    # keeps the macro going (escaped line breaks)
+    assert strip("int/**/x;") == "int x;"
+    mac = "#define M(a) (a) /* two\nlines */ + 1\nint z = M(2);\n"
+    got = strip(mac)
+    assert got.count("\n") == mac.count("\n")
+    assert got.splitlines()[0].endswith("\\") and "+ 1" in got.splitlines()[1]
+    assert strip("int a; /* x\ny */ int b;\n") == "int a;\n int b;\n"
