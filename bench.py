@@ -109,7 +109,7 @@ def parse():
     ap.add_argument("--overlap", type=int, default=-1,
                     help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU; "
                          "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
-                         "+97%% C1, tools/overlap_ab.sh). The roofline's per-launch time then comes from "
+                         "+97%% C1, round 3). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")

@@ -79,3 +79,15 @@ def test_wave_baseline_declines_rm2_rm3(variant, path):
     tabs = scene_compile.compile_scene({}, variant) if path is None else scene_compile.load_scene_file(path, variant)
     o = oracle.Oracle(tabs, abi.default_params(), camera.default_view(64, 36), 64, 36)
     assert o.render_wave(time_schedule(1), rect=(0, 0, 64, 1)) is None
+
+
+@pytest.mark.parametrize("cfg,wave", [("c1", True), ("rm2", False)])
+def test_bench_cpu_leg_fields(cfg, wave):
+    """bench.py's cpu_baseline: the vectorised port for RM1 configs with the scalar oracle timed beside
+    it, the scalar oracle alone for RM2 / RM3."""
+    import bench
+    out = bench.cpu_baseline(bench.CONFIGS[cfg], 4, 0.4, 2, repeats=2)
+    assert out["value"] > 0 and out["cores"] == 2 and out["kind"] == "port"
+    assert ("rmr_cpu_wave.c" in out["implementation"]) == wave
+    assert ("scalar_port" in out) == wave
+    assert len(out["repeats_msamples_per_s"]) == 2

@@ -510,7 +510,7 @@ def test_rm2_shadow_light_bound_bitexact(renderer, max_dist, step_mult):
 def test_culling_switches_full_frame_bitexact(renderer, scene, W, H):
     """The same property at production frame sizes (rare events — NaN directions, near ties, cache
     bounds at grazing angles — show up only over millions of paths): every per-sample radiance of a
-    2-spp frame is bitwise equal with the work-skipping paths on and off (tools/full_frame_sweep.sh
+    2-spp frame is bitwise equal with the work-skipping paths on and off (round 3's full-frame sweep
     runs the other scene families)."""
     path, variant = _cull_scene(scene)
     _setup(renderer, path, variant, W, H, {"max_bounces": 4})

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build librmr.so of a git revision (or of the working tree with "WT") into OUT, for same-process
-# A/B runs with tools/ab.py (each library embeds its own hipRTC source).
+# A/B runs with tools/abrun.py lib:PATH (each library embeds its own hipRTC source).
 #   tools/build_rev.sh REV OUT [EXTRA]      e.g. tools/build_rev.sh HEAD tools/librmr_base.so
 set -e
 REV=$1; OUT=$(realpath -m "$2"); EXTRA=${3:-}
