@@ -1206,31 +1206,17 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
 // (0,-1,0)) never escapes: the reference's map(NaN) "hits" at t = 0 (opU NaN rule).
 // (oxy = o.x + o.y: primary rays pass the host's P.eye_xy, a value the kernel would otherwise keep in a
 // VGPR for the whole launch)
-#ifndef RMR_ESC_PACKED
-#define RMR_ESC_PACKED 1
-#endif
 RMR_D float ray_exit(const KParams& P, V3 o, V3 d, float oxy) {
     const float chk = (oxy + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
     if (!P.esc_on || !(chk == chk)) return __builtin_inff();
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     float last = -__builtin_inff();
-#if RMR_ESC_PACKED
-    // x and y slabs as packed pairs (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations per
-    // component, two per instruction)
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    const f2v oxy2 = {o.x, o.y}, ixy = {ix, iy};
-#endif
     for (int b = 0; b < P.n_esc; b++) {
         // wave-uniform index, constant address space: scalar loads into SGPRs (a generic pointer
         // compiled to per-lane vector loads, one dependent L1 round trip per box)
         CFloat* B = (CFloat*)P.esc_boxes + 6 * b;
-#if RMR_ESC_PACKED
-        const f2v axy = (f2v{B[0], B[1]} - oxy2) * ixy, bxy = (f2v{B[3], B[4]} - oxy2) * ixy;
-        const float ax = axy.x, bx = bxy.x, ay = axy.y, by = bxy.y;
-#else
         const float ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
         const float ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
-#endif
         const float az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
         const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
