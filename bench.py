@@ -207,17 +207,25 @@ def cpu_baseline(cfg, spp, seconds, threads, repeats=3):
             total += done
         return rates, total
 
+    scalar_impl = "scalar C restatement (oracle/rmr_oracle.c)"
+    wave_impl = "AVX2 8-lane wavefront port (oracle/rmr_cpu_wave.c), bitwise the scalar oracle"
     if wave:
         # the vectorised port takes one sample of every sampled row per call (one batch shared by the
-        # threads: a call per row would drain the lanes 40 times as often); the same samples
+        # threads: a call per row would drain the lanes 40 times as often); the same samples. Both
+        # ports are timed (half the budget each) and the faster one is the baseline: on small frames
+        # (C1's 256-pixel rows) the wavefront's lane drain costs more than its vectors gain
         def render(t, rect, first_sample, accum, nthreads):
             return o.render_wave_rows(t, rows, first_sample=first_sample, accum=accum, nthreads=nthreads)
         vunits = [(None, s) for s in range(ns)]
-        rates, total = timed(render, seconds, repeats, vunits, len(rows) * W)
+        wr, wt = timed(render, seconds / 2, repeats, vunits, len(rows) * W)
+        sr, st = timed(o.render, seconds / 2, repeats, units, W)
+        if statistics.median(wr) >= statistics.median(sr):
+            rates, total, impl, other = wr, wt, wave_impl, ("scalar_port", sr, st, scalar_impl)
+        else:
+            rates, total, impl, other = sr, st, scalar_impl, ("wave_port", wr, wt, wave_impl)
     else:
         rates, total = timed(o.render, seconds, repeats, units, W)
-    impl = ("AVX2 8-lane wavefront port (oracle/rmr_cpu_wave.c), bitwise the scalar oracle" if wave
-            else "scalar C restatement (oracle/rmr_oracle.c)")
+        impl, other = scalar_impl, None
     out = {"value": statistics.median(rates), "unit": "Msamples/s", "cores": threads, "kind": "port",
            "per_core": round(statistics.median(rates) / threads, 4), "implementation": impl,
            "repeats_msamples_per_s": [round(x, 4) for x in rates],
@@ -225,15 +233,16 @@ def cpu_baseline(cfg, spp, seconds, threads, repeats=3):
                      "frame x the schedule's first %d samples (%s), %d-thread OpenMP %s; %d threads "
                      "= every CPU of this process's affinity set, capped by OMP_NUM_THREADS (the host-CPU share of "
                      "one GPU on the GPU box)" % (repeats, total, stride, W, H, ns,
-                                                  "one call per sample over all the rows" if wave else
+                                                  "one call per sample over all the rows" if impl == wave_impl else
                                                   "one call per row and sample, rows in bit-reversed order",
                                                   threads, impl, threads),
            "host_cpus_visible": os.cpu_count()}
-    if wave:
-        # the scalar oracle (the checker) on the same work, one short run, for comparison
-        srates, stotal = timed(o.render, max(2.0, seconds / 4), 1, units, W)
-        out["scalar_port"] = {"value": round(srates[0], 4), "per_core": round(srates[0] / threads, 4),
-                              "samples": stotal, "implementation": "scalar C restatement (oracle/rmr_oracle.c)"}
+    if other:
+        # the other port on the same work (the scalar oracle is the checker)
+        out[other[0]] = {"value": round(statistics.median(other[1]), 4),
+                         "per_core": round(statistics.median(other[1]) / threads, 4),
+                         "repeats_msamples_per_s": [round(x, 4) for x in other[1]], "samples": other[2],
+                         "implementation": other[3]}
     ref = LLVMPIPE_PER_VCPU.get(cfg_name_of(cfg))
     if ref:
         # the reference's own path (RayMarch.glsl on Mesa llvmpipe) cannot run on the GPU box (no
