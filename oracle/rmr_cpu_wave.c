@@ -159,11 +159,12 @@ static void start_trace(wctx* c, wave* w, int l, o_v3 eye, o_v3 dir) {
     next_bounce(c, w, l);
 }
 
-/* a fresh sample for lane l (sample_rgb's jittered primary ray, RM1:569-584), or idle */
-static void take_unit(wctx* c, wave* w, int l) {
-    w->phase[l] = W_IDLE;
+/* a fresh sample for the idle lane l (sample_rgb's jittered primary ray, RM1:569-584); false when the
+ * batch has none left. The sample may finish at once (maxBounces 0, maxSteps 0: the lane is idle
+ * again), so callers refill in a loop (refill) rather than by recursion */
+static int take_unit(wctx* c, wave* w, int l) {
     const long u = __atomic_fetch_add(&c->next, 1, __ATOMIC_RELAXED);
-    if (u >= c->total) return;
+    if (u >= c->total) return 0;
     const long pi = u / c->nspp;
     const uint32_t k = (uint32_t)(u % c->nspp);
     const long gi = c->i0 + pi;
@@ -195,9 +196,14 @@ static void take_unit(wctx* c, wave* w, int l) {
         P->L.channels = o3(1.0f, 0.0f, 0.0f);
     }
     start_trace(c, w, l, eye, P->dir0);
+    return 1;
+}
+static void refill(wctx* c, wave* w, int l) {
+    while (w->phase[l] == W_IDLE && take_unit(c, w, l)) {
+    }
 }
 
-/* end of trace(): the sample (or the next separateChannels pass, sample_rgb) */
+/* end of trace(): the sample (or the next separateChannels pass, sample_rgb); the lane is then idle */
 static void finish_trace(wctx* c, wave* w, int l, o_v3 col) {
     wpath* P = &w->p[l];
     if (P->chan >= 0) {
@@ -213,7 +219,7 @@ static void finish_trace(wctx* c, wave* w, int l, o_v3 col) {
     }
     float* r = c->res + 3 * P->unit;
     r[0] = col.x; r[1] = col.y; r[2] = col.z;
-    take_unit(c, w, l);
+    w->phase[l] = W_IDLE;
 }
 
 /* trace_rm1 after march(): hit -> getNormal probes, miss -> sky (RM1:514-561) */
@@ -262,7 +268,7 @@ static const float kProbe[6][3] = {{0.001f, 0.0f, 0.0f},  {-0.001f, -0.0f, -0.0f
 static uint64_t run_chunk(wctx* c) {
     wave w;
     memset(&w, 0, sizeof w);
-    for (int l = 0; l < VW; l++) take_unit(c, &w, l);
+    for (int l = 0; l < VW; l++) refill(c, &w, l);
     const oracle_job* job = c->job;
     const float max_dist = job->params.max_dist, step_mult = job->params.step_multiply;
     const int max_steps = job->params.max_steps;
@@ -336,6 +342,7 @@ static uint64_t run_chunk(wctx* c) {
             ev &= ev - 1;
             if (w.phase[l] == W_NORMAL) shade_hit(c, &w, l);
             else after_march(c, &w, l);
+            refill(c, &w, l);
         }
     }
     return maps;

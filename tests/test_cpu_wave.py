@@ -96,3 +96,16 @@ def test_bench_cpu_leg_fields(cfg, wave):
     else:
         assert "rmr_cpu_wave.c" not in out["implementation"]
     assert len(out["repeats_msamples_per_s"]) == 2
+
+
+def test_wave_baseline_zero_bounce_frame_without_recursion():
+    """maxBounces 0 finishes every sample as soon as it starts: the lanes refill in a loop, not by
+    recursion, so a whole frame's batch does not grow the stack."""
+    W, H = 480, 270
+    prm = abi.default_params(max_bounces=0)
+    o = oracle.Oracle(scene_compile.load_scene_file(os.path.join(SCENES, "cornell5.scene"), "rm1"), prm,
+                      camera.default_view(W, H), W, H)
+    times = time_schedule(8)
+    a = o.render(times, nthreads=2)
+    b = o.render_wave(times, nthreads=1)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
