@@ -31,7 +31,7 @@ def _run(*args, timeout=240):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("gpus,config,spp", [(2, "c2", 4), (3, "c5", 2)])
+@pytest.mark.parametrize("gpus,config,spp", [(2, "c2", 4), (3, "c5", 2), (8, "c2", 2)])
 def test_share_gpu_ranks_reduce_bitexact(gpus, config, spp):
     out = _run("--gpus", str(gpus), "--share-gpu", "--config", config, "--spp", str(spp), "--steps", "3",
                "--warmup", "1", "--no-cpu-baseline", "--no-psnr", "--no-count-pass")
