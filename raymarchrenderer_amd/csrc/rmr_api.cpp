@@ -16,6 +16,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rmr.h"
@@ -130,6 +131,11 @@ struct rmr_ctx {
     // pays one persistent-kernel drain instead of one per 8 GiB
     size_t samp_budget = (size_t)48 << 30;
     std::string err;
+    // capacity of each table buffer (keyed by the address of its device-pointer member): a reload of
+    // the same scene layout (an animation frame) copies into the buffers it has, ordered on the
+    // context's stream, instead of hipFree + hipMalloc, which wait for the whole device — including
+    // another context's frame still rendering (FrameRenderer's two overlapping contexts)
+    std::unordered_map<const void*, size_t> dev_caps;
 };
 
 namespace {
@@ -152,12 +158,27 @@ int fail(rmr_ctx* c, int code, const std::string& m) {
         if (e_ != hipSuccess) return fail(ctx, RMR_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+// Host -> device table upload, ordered on the context's stream: kernels of this context launched
+// before it have read the old contents, those launched after read the new. A buffer is reallocated
+// only when it must grow. The call returns once this context's stream has completed the copy (the
+// source may be a temporary); another context's work on its own stream is not waited for.
 template <class T>
 int dev_upload(rmr_ctx* c, T** dst, const T* src, size_t n) {
-    if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
     const size_t bytes = std::max<size_t>(1, n) * sizeof(T);
-    HIPCHK(c, hipMalloc((void**)dst, bytes));
-    if (n) HIPCHK(c, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    size_t& cap = c->dev_caps[(const void*)dst];
+    if (!*dst || cap < bytes) {
+        if (*dst) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(*dst);
+            *dst = nullptr;
+        }
+        HIPCHK(c, hipMalloc((void**)dst, bytes));
+        cap = bytes;
+    }
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(*dst, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     return RMR_OK;
 }
 
