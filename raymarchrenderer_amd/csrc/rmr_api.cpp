@@ -769,7 +769,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         double eye = 0.0;
         for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));
         const double infl = 0.002 + std::ldexp(eye + 2.0 * E + 3.0 * std::fabs((double)c->params.max_dist), -16);
-        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && std::isfinite(infl) && !c->esc_raw.empty() ? 1 : 0;
+        // (infl < 2^44: |eye|, E, maxDist < 2^60, the range ray_exit's FMA slab form is exact in)
+        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && infl < 0x1p44 && !c->esc_raw.empty() ? 1 : 0;
         if (P.esc_on && infl != c->esc_infl_dev) {
             std::vector<float> bx(c->esc_raw.size());
             for (size_t i = 0; i < bx.size(); i++)   // outward in double, then to float

@@ -87,8 +87,23 @@ RMR_D float div_mk(float a, float b) {
     const float q = a * y;
     return fmaf(fmaf(-b, q, a), y, q);
 }
+// RN(1/b) for every b: rcp_cr where 2^-125 <= |b| <= 2^125 (one unsigned compare on the bits; NaN
+// and inf fail it), the IEEE division only in a wave with a lane outside that range (0, denormal,
+// huge, inf, NaN) — 3 VALU instead of the 10 of div_scale / fmas / fixup
+#ifndef RMR_RCP_FAST
+#define RMR_RCP_FAST 1
+#endif
+RMR_D float rcp_rn(float b) {
+#if RMR_RCP_FAST
+    const bool in = (__float_as_uint(b) & 0x7fffffffu) - 0x01000000u <= 0x7e000000u - 0x01000000u;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!in) == 0, 1)) return rcp_cr(b);
+    return in ? rcp_cr(b) : 1.0f / b;
+#else
+    return 1.0f / b;
+#endif
+}
 RMR_D float length(V3 a) { return sqrt_cr(dot(a, a)); }
-RMR_D V3 normalize(V3 a) { float inv = 1.0f / length(a); return a * inv; }
+RMR_D V3 normalize(V3 a) { float inv = rcp_rn(length(a)); return a * inv; }
 RMR_D V3 vfma(V3 a, float s, V3 b) { return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z)); }
 RMR_D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 RMR_D float fmix(float x, float y, float a) { return fmaf(a, y - x, x); }
@@ -197,6 +212,9 @@ RMR_D float det_acos(float x) {
 }
 
 // ---- log / exp / pow / atan2 (Mandelbulb) ---------------------------------------------------
+#ifndef RMR_LOG_DIVMK
+#define RMR_LOG_DIVMK 1   // det_log's f / (2 + f) by div_mk (tools/probes/logdiv_exhaustive.c: every input)
+#endif
 RMR_D float det_log(float x) {
     if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_huge_valf() : __uint_as_float(0x7fc00000u);
     if (x == __builtin_huge_valf()) return x;
@@ -208,7 +226,14 @@ RMR_D float det_log(float x) {
     u = (u & 0x007fffffu) + 0x3f3504f3u;
     float m = __uint_as_float(u);
     float f = m - 1.0f;
+#if RMR_LOG_DIVMK
+    // f = m - 1 in [-0.293, 0.415] is 0 or a multiple of 2^-24 of magnitude >= 2^-24: the quotient
+    // (|s| <= 0.172) and Markstein's residual (~2^-24 |s|) stay normal, the divisor is in
+    // rcp_cr's range — div_mk is the IEEE quotient here for every input
+    float s = div_mk(f, 2.0f + f);
+#else
     float s = f / (2.0f + f);
+#endif
     float z = s * s;
     float w = z * z;
     float t1 = w * fmaf(w, 0.24279078841f, 0.40000972152f);

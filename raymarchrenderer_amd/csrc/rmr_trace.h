@@ -1206,22 +1206,48 @@ RMR_D V3 sky_color(const KParams& P, V3 dir) {
 // (0,-1,0)) never escapes: the reference's map(NaN) "hits" at t = 0 (opU NaN rule).
 // (oxy = o.x + o.y: primary rays pass the host's P.eye_xy, a value the kernel would otherwise keep in a
 // VGPR for the whole launch)
+// Slab parameters as one FMA each, B ix - o ix (o ix once per ray; RMR_ESC_FMA=0: (B - o) ix
+// always, A/B). With ix = RN-ish(1/d_k) (v_rcp, <= 1 ulp) the parameter t' of a face B satisfies
+// |(o + t' d)_k - B| <= 2^-22.4 |B - o_k| + 2^-24 |o_k| <= 2^-21 (|B| + |o|) whatever d_k is (t's
+// error grows as 1 / |d_k|, the offset it causes along axis k shrinks as |d_k|): every point past a
+// computed far face, or on a ray whose computed slab interval is empty, is outside the box shrunk
+// by that much, far inside the inflation's 2^-16 (|eye| + 2E + 3 maxDist) term. The products stay
+// finite: |B|, |o| < 2^60 (the host turns the bound off beyond) and |ix| <= 2^40; a wave with a lane
+// whose direction has a component below ~2^-40 (its ix may be +-inf, and inf - inf a NaN on one
+// side of a slab only) takes the (B - o) ix form, whose infinities carry the right signs.
+#ifndef RMR_ESC_FMA
+#define RMR_ESC_FMA 1
+#endif
+RMR_D void esc_box(float& last, float ax, float bx, float ay, float by, float az, float bz) {
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    // inside this box for t in [tn, tf] (nonempty and ahead): the ray may still hit its primitives
+    if (!(tn > tf)) last = fmaxf(last, tf);
+}
 RMR_D float ray_exit(const KParams& P, V3 o, V3 d, float oxy) {
     const float chk = (oxy + (o.z + d.x)) + (d.y + d.z);   // NaN if any is NaN (or +-inf mix)
     if (!P.esc_on || !(chk == chk)) return __builtin_inff();
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     float last = -__builtin_inff();
-    for (int b = 0; b < P.n_esc; b++) {
-        // wave-uniform index, constant address space: scalar loads into SGPRs (a generic pointer
-        // compiled to per-lane vector loads, one dependent L1 round trip per box)
-        CFloat* B = (CFloat*)P.esc_boxes + 6 * b;
-        const float ax = (B[0] - o.x) * ix, bx = (B[3] - o.x) * ix;
-        const float ay = (B[1] - o.y) * iy, by = (B[4] - o.y) * iy;
-        const float az = (B[2] - o.z) * iz, bz = (B[5] - o.z) * iz;
-        const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-        const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-        // inside this box for t in [tn, tf] (nonempty and ahead): the ray may still hit its primitives
-        if (!(tn > tf)) last = fmaxf(last, tf);
+    // wave-uniform box index, constant address space: scalar loads into SGPRs (a generic pointer
+    // compiled to per-lane vector loads, one dependent L1 round trip per box)
+#if RMR_ESC_FMA
+    const float im = fmaxf(fmaxf(fabsf(ix), fabsf(iy)), fabsf(iz));
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(im <= 0x1p40f)) == 0, 1)) {
+        const float ox = -(o.x * ix), oy = -(o.y * iy), oz = -(o.z * iz);
+        for (int b = 0; b < P.n_esc; b++) {
+            CFloat* B = (CFloat*)P.esc_boxes + 6 * b;
+            esc_box(last, fmaf(B[0], ix, ox), fmaf(B[3], ix, ox), fmaf(B[1], iy, oy), fmaf(B[4], iy, oy),
+                    fmaf(B[2], iz, oz), fmaf(B[5], iz, oz));
+        }
+    } else
+#endif
+    {
+        for (int b = 0; b < P.n_esc; b++) {
+            CFloat* B = (CFloat*)P.esc_boxes + 6 * b;
+            esc_box(last, (B[0] - o.x) * ix, (B[3] - o.x) * ix, (B[1] - o.y) * iy, (B[4] - o.y) * iy,
+                    (B[2] - o.z) * iz, (B[5] - o.z) * iz);
+        }
     }
     // relative error < 2^-21: widen a positive bound
     return last > 0.0f ? fmaf(last, 1.0f + 0x1p-19f, 0x1p-60f) : last;
