@@ -126,6 +126,20 @@ RMR_D float div_314(float x) {
     const float r = fmaf(-q0, y, x);
     return fmaf(r, rc, q0);
 }
+// x / c for a literal c by the same two FMAs (RN(1/c) folded at compile time), where the caller's
+// x range is checked against the IEEE quotient (tools/probes/wl_divconst_check.c; RMR_DIV_K=0: IEEE)
+#ifndef RMR_DIV_K
+#define RMR_DIV_K 1
+#endif
+RMR_D float div_k(float x, float c) {
+#if RMR_DIV_K
+    const float rc = 1.0f / c;
+    const float q0 = x * rc;
+    return fmaf(fmaf(-q0, c, x), rc, q0);
+#else
+    return x / c;
+#endif
+}
 RMR_D float mod_314(float x) { return fmaf(-3.14f, floorf(div_314(x)), x); }
 RMR_D V3 reflect(V3 I, V3 N) { float k = 2.0f * dot(N, I); return vfma(N, -k, I); }
 RMR_D V3 refract(V3 I, V3 N, float eta) {

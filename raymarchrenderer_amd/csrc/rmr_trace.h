@@ -1355,17 +1355,19 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
         }
         if (VAR == RMR_VARIANT_RM3) {
             // wavelengthToColor(range) * power, RM3:447-522 / 540
+            // wl is an integer: each quotient by a constant is the two-FMA form, equal to the IEEE one on
+            // every numerator of its branch (tools/probes/wl_divconst_check.c)
             float wl = (float)L.wl, R, G, B, alpha;
-            if (wl >= 380.0f && wl < 440.0f) { R = (-1.0f * (wl - 440.0f)) / 60.0f; G = 0.0f; B = 1.0f; }
-            else if (wl >= 440.0f && wl < 490.0f) { R = 0.0f; G = (wl - 440.0f) / 50.0f; B = 1.0f; }
-            else if (wl >= 490.0f && wl < 510.0f) { R = 0.0f; G = 1.0f; B = (-1.0f * (wl - 510.0f)) / 20.0f; }
-            else if (wl >= 510.0f && wl < 580.0f) { R = (wl - 510.0f) / 70.0f; G = 1.0f; B = 0.0f; }
-            else if (wl >= 580.0f && wl < 645.0f) { R = 1.0f; G = (-1.0f * (wl - 645.0f)) / 65.0f; B = 0.0f; }
+            if (wl >= 380.0f && wl < 440.0f) { R = div_k(-1.0f * (wl - 440.0f), 60.0f); G = 0.0f; B = 1.0f; }
+            else if (wl >= 440.0f && wl < 490.0f) { R = 0.0f; G = div_k(wl - 440.0f, 50.0f); B = 1.0f; }
+            else if (wl >= 490.0f && wl < 510.0f) { R = 0.0f; G = 1.0f; B = div_k(-1.0f * (wl - 510.0f), 20.0f); }
+            else if (wl >= 510.0f && wl < 580.0f) { R = div_k(wl - 510.0f, 70.0f); G = 1.0f; B = 0.0f; }
+            else if (wl >= 580.0f && wl < 645.0f) { R = 1.0f; G = div_k(-1.0f * (wl - 645.0f), 65.0f); B = 0.0f; }
             else if (wl >= 645.0f && wl <= 780.0f) { R = 1.0f; G = 0.0f; B = 0.0f; }
             else { R = 0.0f; G = 0.0f; B = 0.0f; }
             if (wl > 780.0f || wl < 380.0f) alpha = 0.0f;
-            else if (wl > 700.0f) alpha = (780.0f - wl) / 80.0f;
-            else if (wl < 420.0f) alpha = (wl - 380.0f) / 40.0f;
+            else if (wl > 700.0f) alpha = div_k(780.0f - wl, 80.0f);
+            else if (wl < 420.0f) alpha = div_k(wl - 380.0f, 40.0f);
             else alpha = 1.0f;
             const V3 c = (v3(R, G, B) * alpha) * L.power;
             P.samp[L.unit] = make_float4(c.x, c.y, c.z, 1.0f);
