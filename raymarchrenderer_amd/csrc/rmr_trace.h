@@ -319,23 +319,47 @@ struct MBStep {
     int i;
     bool fin;   // estimator finished: waits for the next finishing batch
 };
-RMR_D void mb_begin(MBStep& s, V3 p0, int iters) {
+// The loop's bailout test runs at the end of each iteration (and in mb_begin for the first), not at
+// the start of the next step: a lane whose point is outside the bailout radius (most march points:
+// 0.92 iterations per map) is finished from mb_begin on and joins the next finishing
+// batch without a pass, and a bailing lane finishes in the pass of its last iteration. The same
+// operations in the same order per lane (RMR_MB_EARLY=0: the test at the start of mb_step, A/B).
+#ifndef RMR_MB_EARLY
+#define RMR_MB_EARLY 1
+#endif
+RMR_D void mb_begin(MBStep& s, V3 p0, int iters, float bail) {
     s.z = p0;
     s.p0 = p0;
     s.dr = 1.0f;
     s.r = 0.0f;   // (iters <= 0: the loop does not run, r stays 0)
     s.i = 0;
     s.fin = iters <= 0;
+#if RMR_MB_EARLY
+    if (!s.fin) {
+        s.r = length(s.z);
+        s.fin = s.r > bail;
+    }
+#else
+    (void)bail;
+#endif
 }
 RMR_D bool mb_step(MBStep& s, float power, int iters, float bail, unsigned long long* cnt) {
     (void)cnt;
     const V3 p0 = s.p0;
+#if !RMR_MB_EARLY
     s.r = length(s.z);
     if (s.r > bail) return true;
+#endif
     RMR_COUNT_MB(cnt, active_lanes(), power);
     mb_iter(s.z, s.dr, p0, power, s.r);
     s.i++;
+#if RMR_MB_EARLY
+    if (s.i >= iters) return true;   // r: the last |z| tested, as the loop leaves it
+    s.r = length(s.z);
+    return s.r > bail;
+#else
     return s.i >= iters;
+#endif
 }
 // lanes finishing their estimator accumulate until RMR_MB_FIN of them (or every running lane) have
 // finished; then the rest of their map() runs once for all of them
