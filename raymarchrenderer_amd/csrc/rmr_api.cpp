@@ -432,8 +432,8 @@ int ensure_jit(rmr_ctx* c) {
     int b = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, k.fn, k.block, 0) != hipSuccess || b <= 0) b = 4;
     k.blocks_per_cu = b;
-    // shading batch per kernel class (rmr_jit.hpp JitFacts::shade_t). Measured: the Mandelbulb 8 (C3
-    // +2-3%); RM1 inline sphere/box maps 16 (20 until the map() loop lost ~12% of its instructions in
+    // shading batch per kernel class (rmr_jit.hpp JitFacts::shade_t). Measured: the Mandelbulb 10 (8
+    // until round 5's early bailout made the passes cheaper: 10 -0.6%, csg_nodes -0.5%); RM1 inline sphere/box maps 16 (20 until the map() loop lost ~12% of its instructions in
     // round 2; then 14-16 best on Cornell-5, 20 -> 16: -2.4%, multilight -4%, default +1.2%); node-program
     // materials 20 (round 4, 1080p 16 spp: default.scene 27.9 -> 26.9 ms, multilight 13.41 -> 13.24; 24:
     // -6% / +1.4%); the cache kernels 20 (csg256 1080p 8 spp: 16.83 -> 16.68 ms; 24: 16.81); the

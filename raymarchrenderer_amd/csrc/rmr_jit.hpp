@@ -50,10 +50,10 @@ struct JitFacts {
     bool cache = false, general = false, prog = false, cert = false;
     int chunk() const { return cache ? 64 : 128; }   // rmr_trace.h RMR_CHUNK_CACHE / RMR_CHUNK
     // default shading batch: general maps without material programs, whose map() dwarfs the shading
-    // (the Mandelbulb): 8 (C3 +2-3%); node-program materials, the cache kernels and the certified
+    // (the Mandelbulb): 10 (C3: 8 / 12 within 0.6%, 6 / 16 +3%, profiles/r05_c3_shade_ab.log); node-program materials, the cache kernels and the certified
     // sphere/box kernels (their batches run the certified probes): 20; otherwise 16 (rmr_api.cpp)
     int shade_t() const {
-        if (variant == RMR_VARIANT_RM1 && general && !prog) return 8;
+        if (variant == RMR_VARIANT_RM1 && general && !prog) return 10;
         if (prog || cache || cert) return 20;
         return 16;
     }
