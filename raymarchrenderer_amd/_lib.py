@@ -118,6 +118,8 @@ def lib(diag=None):
         "rmr_candidate_grid": (C.c_int, [fp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                          C.POINTER(C.c_int32), fp, C.POINTER(C.c_uint32), C.c_size_t,
                                          C.POINTER(C.c_uint16), C.c_size_t]),
+        # diagnostic library only (rmr_api.cpp RMR_DIAG): ray_exit at given rays
+        "rmr_diag_ray_exit": (C.c_int, [vp, fp, C.c_int, fp, fp, C.c_int, ip]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):   # (an older build given by path may lack a newer entry point)

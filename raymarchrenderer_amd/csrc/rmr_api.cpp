@@ -28,6 +28,7 @@
 namespace rmr {
 hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool persistent, int grid, hipStream_t s);
 hipError_t launch_fold(const KParams& P, hipStream_t s);
+hipError_t launch_ray_exit(const KParams& P, const float* rays, float* out, int n, hipStream_t s);
 hipError_t launch_display(const float4* accum, int img_w, int img_h, float cx, float cy, float zoom, float min_x,
                           float min_y, float max_x, float max_y, int scr_w, int scr_h, uint32_t* rgba8,
                           const float* thr, hipStream_t s);
@@ -699,6 +700,36 @@ int collect_timing(rmr_ctx* c) {
     return RMR_OK;
 }
 
+// The launch's escape bound (rmr_trace.h ray_exit): the escape boxes inflated by 0.002 + 2^-16 (|eye| +
+// 2E + 3 maxDist) >= 0.001 + 8 x the float error of a distance at any point a march reaches
+// (|p| <= |eye| + E + 3 maxDist) + the rounding of the slab parameters
+int escape_params(rmr_ctx* c, KParams& P) {
+    const CompiledScene& s = c->scene;
+    bool simple = !s.prims.empty();
+    double E = 0.0;
+    for (const rmr_prim& q : s.prims) {
+        simple = simple && escape_prim(q);
+        if (!escape_prim(q)) continue;
+        for (int k = 0; k < 3; k++) E = std::max(E, std::fabs((double)q.c[k]) + (double)escape_halfwidth(q, k));
+    }
+    double eye = 0.0;
+    for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));
+    const double infl = 0.002 + std::ldexp(eye + 2.0 * E + 3.0 * std::fabs((double)c->params.max_dist), -16);
+    // (infl < 2^44: |eye|, E, maxDist < 2^60, the range ray_exit's FMA slab form is exact in)
+    P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && infl < 0x1p44 && !c->esc_raw.empty() ? 1 : 0;
+    if (P.esc_on && infl != c->esc_infl_dev) {
+        std::vector<float> bx(c->esc_raw.size());
+        for (size_t i = 0; i < bx.size(); i++)   // outward in double, then to float
+            bx[i] = (float)((double)c->esc_raw[i] + ((i % 6) < 3 ? -infl : infl));
+        int rr;
+        if ((rr = dev_upload(c, &c->d_esc, bx.data(), bx.size()))) return rr;
+        c->esc_infl_dev = infl;
+    }
+    P.esc_boxes = c->d_esc;
+    P.n_esc = (int)(c->esc_raw.size() / 6);
+    return RMR_OK;
+}
+
 // Core: nspp samples over an 8x8 tile list, clipped to [x0,x1)x[y0,y1).
 int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, int x1, int y1,
                  const float* times, uint32_t first_sample, uint32_t nspp) {
@@ -756,31 +787,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     }
     P.full_threshold = c->full_threshold;
     {
-        // escape bound (rmr_trace.h ray_exit): the escape boxes inflated by 0.002 + 2^-16 (|eye| + 2E +
-        // 3 maxDist) >= 0.001 + 8 x the float error of a distance at any point a march reaches
-        // (|p| <= |eye| + E + 3 maxDist) + the rounding of the slab parameters
-        bool simple = !s.prims.empty();
-        double E = 0.0;
-        for (const rmr_prim& q : s.prims) {
-            simple = simple && escape_prim(q);
-            if (!escape_prim(q)) continue;
-            for (int k = 0; k < 3; k++) E = std::max(E, std::fabs((double)q.c[k]) + (double)escape_halfwidth(q, k));
-        }
-        double eye = 0.0;
-        for (int k = 0; k < 3; k++) eye = std::max(eye, std::fabs((double)c->view[k]));
-        const double infl = 0.002 + std::ldexp(eye + 2.0 * E + 3.0 * std::fabs((double)c->params.max_dist), -16);
-        // (infl < 2^44: |eye|, E, maxDist < 2^60, the range ray_exit's FMA slab form is exact in)
-        P.esc_on = (c->cull & RMR_CULL_ESCAPE) && simple && infl < 0x1p44 && !c->esc_raw.empty() ? 1 : 0;
-        if (P.esc_on && infl != c->esc_infl_dev) {
-            std::vector<float> bx(c->esc_raw.size());
-            for (size_t i = 0; i < bx.size(); i++)   // outward in double, then to float
-                bx[i] = (float)((double)c->esc_raw[i] + ((i % 6) < 3 ? -infl : infl));
-            int rr;
-            if ((rr = dev_upload(c, &c->d_esc, bx.data(), bx.size()))) return rr;
-            c->esc_infl_dev = infl;
-        }
-        P.esc_boxes = c->d_esc;
-        P.n_esc = (int)(c->esc_raw.size() / 6);
+        int rr;
+        if ((rr = escape_params(c, P))) return rr;
     }
     {
         // primary rays' first march step from the eye (rmr_trace.h eye_map): the march point
@@ -1491,6 +1499,38 @@ int rmr_trace_samples(rmr_ctx* c, const float* times, int x0, int y0, int x1, in
             }
     return rmr_write_accum(c, keep.data(), keep.size() * sizeof(float));
 }
+
+#if RMR_DIAG
+// Diagnostic library only (not in include/rmr.h): the escape bound ray_exit at n given rays (rays:
+// o.xyz, d.xyz per ray) with the context's scene, view and maxDist, as a launch would use it; out[i]
+// = the bound (+inf: none). boxes (optional, 6 floats per box, up to max_boxes) receives the inflated
+// escape boxes the kernel read, *n_boxes their number (0: the bound is off for this scene).
+int rmr_diag_ray_exit(rmr_ctx* c, const float* rays, int n, float* out, float* boxes, int max_boxes, int* n_boxes) {
+    if (!c->scene_loaded) return fail(c, RMR_E_STATE, "no scene loaded");
+    if (n < 0 || (n > 0 && (!rays || !out))) return fail(c, RMR_E_INVALID, "bad rays / out");
+    if (!c->view_set) default_view(c);
+    KParams P{};
+    int rr;
+    if ((rr = escape_params(c, P))) return rr;
+    if (n_boxes) *n_boxes = P.esc_on ? P.n_esc : 0;
+    if (boxes && P.esc_on && max_boxes > 0) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(boxes, c->d_esc, sizeof(float) * 6 * (size_t)std::min(max_boxes, P.n_esc), hipMemcpyDeviceToHost));
+    }
+    if (n == 0) return RMR_OK;
+    float *d_rays = nullptr, *d_out = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d_rays, sizeof(float) * 6 * (size_t)n));
+    HIPCHK(c, hipMalloc((void**)&d_out, sizeof(float) * (size_t)n));
+    hipError_t e = hipMemcpyAsync(d_rays, rays, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = rmr::launch_ray_exit(P, d_rays, d_out, n, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_out);
+    HIPCHK(c, e);
+    return RMR_OK;
+}
+#endif
 
 int rmr_abi_sizes(int32_t* out, int n) {
     const int32_t s[] = {(int32_t)sizeof(rmr_prim), (int32_t)sizeof(rmr_op), (int32_t)sizeof(rmr_material),

@@ -50,6 +50,19 @@ hipError_t launch_trace(const KParams& P, int variant, int np, bool prog, bool p
     }
     return hipGetLastError();
 }
+// ray_exit at given rays (o.xyz, d.xyz per ray), with the launch's escape boxes: the diagnostic
+// library's rmr_diag_ray_exit (tests/test_gpu_escape_bound.py checks the bound's validity)
+__global__ void k_ray_exit(KParams P, const float* rays, float* out, int n) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) {
+        const float* r = rays + 6 * (size_t)i;
+        out[i] = ray_exit(P, v3(r[0], r[1], r[2]), v3(r[3], r[4], r[5]));
+    }
+}
+hipError_t launch_ray_exit(const KParams& P, const float* rays, float* out, int n, hipStream_t s) {
+    k_ray_exit<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(P, rays, out, n);
+    return hipGetLastError();
+}
 hipError_t launch_fold(const KParams& P, hipStream_t s) {
     const uint64_t threads = (uint64_t)P.n_tiles * 64;
     k_fold<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(P);

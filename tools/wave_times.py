@@ -18,8 +18,10 @@ ap.add_argument("--spp", default="8,64")
 ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "cornell5.scene"))
 ap.add_argument("--bounces", type=int, default=4)
 ap.add_argument("--variant", default="rm1", help="rm1 / rm2 / rm3 (rm3: --scene builtin)")
+ap.add_argument("--W", type=int, default=1920)
+ap.add_argument("--H", type=int, default=1080)
 a = ap.parse_args()
-r = Renderer(0, 1920, 1080)
+r = Renderer(0, a.W, a.H)
 r.set_jit(1)
 if a.scene == "builtin":
     r.load_builtin(a.variant)
@@ -40,5 +42,6 @@ for s in [int(x) for x in a.spp.split(",")]:
     print(json.dumps({"spp": s, "trace_ms": round(st.trace_ms, 3), "launches": int(st.trace_launches),
                       "first_exhaust_us": us(M ^ c[11]), "last_exhaust_us": us(c[10]),
                       "first_end_us": us(M ^ c[12]), "last_end_us": us(c[13]),
-                      "mean_drain_us": round(c[15] / 100.0 / max(1, 8192), 1)}), flush=True)
+                      "mean_drain_us": round(c[15] / 100.0 / max(1, 8192), 1), "label": "%s %dx%d" % (
+                          os.path.basename(a.scene), a.W, a.H)}), flush=True)
 r.close()
