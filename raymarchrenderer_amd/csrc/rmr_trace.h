@@ -781,6 +781,36 @@ RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j) {
 RMR_D float prim_dist(const KParams& P, int k, V3 p, float& mid, int& j) {
     return prim_dist_at((const float4*)(P.dprims + k), p, mid, j);
 }
+// The LDS copy of the table without per-lane selects (hipRTC cache kernels whose table is in LDS and
+// whose material ids all carry a scene index in their low mantissa bits, am_pack; rmr_jit.cpp emits
+// RMR_NPC_PACKED): a = (c.xyz, sphere ? r : 0), b = (box ? r.xyz : 0, am_pack(mat_id, j)). The same
+// operations as prim_dist_at on the values it selects (a sphere is the box of half-extent 0 minus its
+// radius, a box subtracts 0), so the same bits; a.xyzw of a sphere stays (c, r) for am_sphere_at.
+#ifndef RMR_NPC_PACKED
+#define RMR_NPC_PACKED 0
+#endif
+constexpr bool kNpcPacked = RMR_NPC_PACKED && RMR_NPC_DP_LDS == 1;
+RMR_D void npc_pack_entry(float4& a, float4& b) {
+    const int tw = __float_as_int(b.z);
+    const bool box = (tw & 0xff) == RMR_PRIM_BOX;
+    const float4 na = make_float4(a.x, a.y, a.z, box ? 0.0f : a.w);
+    const float4 nb = make_float4(box ? a.w : 0.0f, box ? b.x : 0.0f, box ? b.y : 0.0f, am_pack(b.w, tw >> 8));
+    a = na;
+    b = nb;
+}
+RMR_D float prim_dist_packed(const float4* q, V3 p, float& mid, int& j) {
+    const float4 a = q[0], b = q[1];
+    mid = am_id_of(b.w);
+    j = am_w_of(b.w);
+    const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - v3(b.x, b.y, b.z);
+    const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
+    return (k0 + length(vmax0(qq))) - a.w;
+}
+// prim_dist_at on the table the cache kernel reads (dtab / the LDS copy)
+RMR_D float prim_dist_tab(const float4* q, V3 p, float& mid, int& j) {
+    if constexpr (kNpcPacked) return prim_dist_packed(q, p, mid, j);
+    else return prim_dist_at(q, p, mid, j);
+}
 // Primitives per lane in the nearest-primitive cache (1 or 2): with 2 the cache holds the two
 // nearest primitives and bounds every other one (a ray passing between two neighbours keeps them).
 #ifndef RMR_NPC_K
@@ -1033,7 +1063,15 @@ RMR_D float am_sphere_at(const float4* q, V3 p) {
 #ifndef RMR_NPC_SPHERES
 #define RMR_NPC_SPHERES 0   // 1: every primitive a grid cell lists is a sphere (rmr_jit.cpp)
 #endif
-#define RMR_AM_LISTED(q, p) (RMR_NPC_SPHERES ? am_sphere_at((q), (p)) : am_prim_at((q), (p)))
+// am_prim_at on the packed LDS table (kNpcPacked)
+RMR_D float am_prim_packed(const float4* q, V3 p) {
+    const float4 a = q[0], b = q[1];
+    const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - v3(b.x, b.y, b.z);
+    const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
+    const V3 o = vmax0(qq);
+    return (k0 + __builtin_amdgcn_sqrtf(dot(o, o))) - a.w;
+}
+#define RMR_AM_LISTED(q, p) (RMR_NPC_SPHERES ? am_sphere_at((q), (p)) : (kNpcPacked ? am_prim_packed((q), (p)) : am_prim_at((q), (p))))
 // dtab: the leaf-ordered primitive table as float4 pairs (the LDS copy of trace_main when it has one)
 RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int ks, int js, float ds, float ms,
                       const float4* dtab) {
@@ -1131,7 +1169,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         if (uniq) {
             float mid;
             int j;
-            const float dw = (k1 == ks) ? ds : prim_dist_at(dtab + 2 * k1, p, mid, j);
+            const float dw = (k1 == ks) ? ds : prim_dist_tab(dtab + 2 * k1, p, mid, j);
             if (k1 == ks) mid = ms;
             opu(d, dw, mid);
             kw = (dw > P.max_dist) ? -1 : k1;
@@ -1677,7 +1715,7 @@ RMR_D void cert_normals(const KParams& P, Lane& L, bool mine, uint64_t cm, int* 
         const V3 e = v3(sg * (ax == 0 ? 0.001f : 0.0f), sg * (ax == 1 ? 0.001f : 0.0f), sg * (ax == 2 ? 0.001f : 0.0f));
         float mid;
         int j;
-        const float F = prim_dist_at(dtab + 2 * (act ? w : 0), v3(hx, hy, hz) + e, mid, j);
+        const float F = prim_dist_tab(dtab + 2 * (act ? w : 0), v3(hx, hy, hz) + e, mid, j);
         const float val = (P.max_dist >= F) ? F : P.max_dist;   // opu(d = (maxDist, -1), F, .).x
 #pragma unroll
         for (int k = 0; k < 6; k++) {   // owners collect the values of this pass
@@ -2307,10 +2345,19 @@ RMR_D void trace_main(const KParams& P) {
     __shared__ float s_rng[kSeeds ? 3 : 1][4][kSeeds ? 64 : 1];
     const bool dp_lds = MAP::kCache && (RMR_NPC_DP_LDS >= 0 ? RMR_NPC_DP_LDS == 1 : P.n_prims <= RMR_NPC_LDS_MAX);
     if (dp_lds) {
-        for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
+        if constexpr (kNpcPacked) {
+            for (int i = (int)threadIdx.x; i < P.n_prims; i += (int)blockDim.x) {
+                float4 a = ((const float4*)P.dprims)[2 * i], b = ((const float4*)P.dprims)[2 * i + 1];
+                npc_pack_entry(a, b);
+                s_dp[2 * i] = a;
+                s_dp[2 * i + 1] = b;
+            }
+        } else {
+            for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
+        }
         __syncthreads();
     }
-#define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_at(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
+#define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_tab(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
 #define RMR_DTAB (dp_lds ? (const float4*)s_dp : (const float4*)P.dprims)
     const int wv = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);   // the wave's index in its block (an SGPR)
     uint32_t chunk_base = 0;
