@@ -675,3 +675,49 @@ def test_jit_stepped_mandelbulb_source(tmp_path, monkeypatch):
     # a sphere/box scene has no stepped map
     k_c5 = jit_compile_scene(os.path.join(SCENES, "cornell5.scene"), "rm1", diag=True)
     assert "kStepped = false" in (tmp_path / "d" / (k_c5 + ".hip")).read_text()
+
+
+def _csg64_unpackable(tmp_path):
+    """csg64 with one object's material id out of am_pack's range (|id| >= 2^15, no such material:
+    the path ends black, as in the reference): the cache kernel then keeps the LDS table unpacked."""
+    import json
+    s = json.load(open(os.path.join(SCENES, "csg64.scene")))
+    s["objects"][5]["matID"] = 40000
+    p = tmp_path / "csg64_unpackable.scene"
+    p.write_text(json.dumps(s))
+    return str(p)
+
+
+@pytest.mark.parametrize("unpackable", [False, True])
+def test_cache_kernel_packed_table_only_for_packable_ids(tmp_path, monkeypatch, unpackable):
+    """rmr_jit.cpp emits RMR_NPC_PACKED (the select-free LDS primitive table, rmr_trace.h
+    npc_pack_entry) for a cache scene only when every material id can carry a scene index."""
+    path = _csg64_unpackable(tmp_path) if unpackable else os.path.join(SCENES, "csg64.scene")
+    dump = tmp_path / "dump"
+    dump.mkdir()
+    monkeypatch.setenv("RMR_JIT_CACHE", str(tmp_path / "cache"))
+    monkeypatch.setenv("RMR_JIT_DUMP", str(dump))
+    key = jit_compile_scene(path, "rm1", diag=True)
+    src = (dump / (key + ".hip")).read_text()
+    assert "#define RMR_NPC_DP_LDS 1" in src
+    assert ("#define RMR_NPC_PACKED 1" in src) == (not unpackable)
+
+
+@pytest.mark.gpu
+def test_cache_kernel_unpacked_table_bitexact_vs_oracle(renderer, tmp_path):
+    """The cache kernel on the unpacked LDS table (a material id am_pack cannot carry) against the
+    oracle, every sample of a small frame (the packed table: rm1_csg64_b4 above)."""
+    path = _csg64_unpackable(tmp_path)
+    W, H = 44, 36
+    rect = (3, 2, 41, 35)
+    prm, view = _setup(renderer, path, "rm1", W, H, {"max_bounces": 4})
+    renderer.set_jit(1)
+    try:
+        times = time_schedule(3, frame=2)
+        gpu = renderer.trace_samples(times, rect)
+    finally:
+        renderer.set_jit(2)
+    cpu = oracle.Oracle(_tables(path, "rm1"), prm, view, W, H).trace_samples(times, rect)
+    a, b = gpu[..., :3], cpu[..., :3]
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), "%d samples differ" % (~same.all(-1)).sum()
