@@ -111,6 +111,11 @@ def parse():
                          "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
                          "+97%% C1, round 3). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
+    ap.add_argument("--tile-order", choices=["cost", "rows"], default="cost",
+                    help="cost: each rank hands its costliest 32x32 tiles out first where tile costs are uneven "
+                         "(a 2-sample probe of every tile's map() evaluations before the timed region, "
+                         "FrameRenderer.order_tiles_by_cost: the launches' drains end on cheap tiles; C3 +2.7%%, "
+                         "the others unchanged; same image bits); rows: row-major")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
     ap.add_argument("--share-gpu", action="store_true",
@@ -517,6 +522,8 @@ def predict_partition(args, cfg):
 
     def timed(tile, rank, world, nspp):
         fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams)
+        if args.tile_order == "cost":
+            fr.order_tiles_by_cost(time_schedule(2))
         f = [0]
 
         def step():
@@ -638,6 +645,7 @@ def main():
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_acc)]
     torch.cuda.synchronize()
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
+    tiles_reordered = fr.order_tiles_by_cost(time_schedule(2)) if args.tile_order == "cost" else False
     static_times = time_schedule(spp)
     frame_no = [0]
     last = {}
@@ -794,7 +802,8 @@ def main():
                                       % (cfg["name"], {"rm1": "RayMarch.glsl", "rm2": "RayMarch2.glsl",
                                                        "rm3": "RayMarch3.glsl"}[variant_of(cfg)], W, H, spp, BOUNCES),
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
-                          "samples_per_step": W * H * spp, "tile": TILE, "parallelism": "tiles%d" % world,
+                          "samples_per_step": W * H * spp, "tile": TILE, "tile_order": "cost" if tiles_reordered else "rows",
+                          "parallelism": "tiles%d" % world,
                           "frame_streams": n_ctx},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity,
                "reference_equivalent_work": work_ref}

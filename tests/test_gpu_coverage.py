@@ -270,3 +270,41 @@ def test_render_tiles_rejects_repeated_tiles(renderer):
     with pytest.raises(RMRError):
         renderer.render_tiles(time_schedule(1), [(-1, 0)], 32)
     renderer.render_tiles(time_schedule(1), [(0, 0), (1, 1)], 32)
+
+
+@pytest.mark.parametrize("scene", ["mandelbulb.scene", "cornell5.scene"])
+def test_frame_renderer_cost_ordered_tiles_same_frame(scene):
+    """FrameRenderer.order_tiles_by_cost (the bench's default tile order): the costliest tiles first by
+    a probe of each tile's map() evaluations; the probe's writes into the first accumulator do not
+    reach the frame, and the frame is the row-major frame bit for bit."""
+    import torch
+    from raymarchrenderer_amd import Renderer
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer, frame_tiles, tile_costs
+    W, H, tile = 192, 128, 32
+    path = os.path.join(SCENES, scene)
+    r = Renderer(0, W, H)
+    ref = Renderer(0, W, H)
+    try:
+        for x in (r, ref):
+            _setup(x, path, W, H, max_bounces=2)
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        fr = FrameRenderer(r, acc, W, H, tile, 0, 1)
+        rows = np.array(frame_tiles(W, H, tile), np.int32)
+        reordered = fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0)
+        cost = tile_costs(ref, rows, tile, time_schedule(2))
+        assert reordered
+        assert sorted(map(tuple, fr.tiles.tolist())) == sorted(map(tuple, rows.tolist()))
+        want_order = rows[np.argsort(-cost, kind="stable")]
+        assert np.array_equal(fr.tiles, want_order)
+        assert cost.max() > cost.min()
+        times = time_schedule(4, frame=3)
+        out = fr.frame(times)
+        with torch.cuda.stream(fr.streams[0]):
+            got = out.to("cpu", non_blocking=False).numpy().copy()
+        ref.reload()
+        ref.render_tiles(times, rows, tile)
+        want = ref.read_accum()
+        assert _same(got, want).all()
+    finally:
+        r.close()
+        ref.close()
