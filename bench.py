@@ -111,11 +111,12 @@ def parse():
                          "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
                          "+97%% C1, round 3). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
-    ap.add_argument("--tile-order", choices=["cost", "rows"], default="cost",
+    ap.add_argument("--tile-order", choices=["cost", "rows", "cost-always"], default="cost",
                     help="cost: each rank hands its costliest 32x32 tiles out first where tile costs are uneven "
                          "(a 2-sample probe of every tile's map() evaluations before the timed region, "
                          "FrameRenderer.order_tiles_by_cost: the launches' drains end on cheap tiles; C3 +2.7%%, "
-                         "the others unchanged; same image bits); rows: row-major")
+                         "the others unchanged; same image bits); rows: row-major; cost-always: cost order "
+                         "whatever the spread (experiments)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
     ap.add_argument("--share-gpu", action="store_true",
@@ -522,8 +523,8 @@ def predict_partition(args, cfg):
 
     def timed(tile, rank, world, nspp):
         fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams)
-        if args.tile_order == "cost":
-            fr.order_tiles_by_cost(time_schedule(2))
+        if args.tile_order != "rows":
+            fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
         f = [0]
 
         def step():
@@ -645,7 +646,8 @@ def main():
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_acc)]
     torch.cuda.synchronize()
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
-    tiles_reordered = fr.order_tiles_by_cost(time_schedule(2)) if args.tile_order == "cost" else False
+    tiles_reordered = (fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
+                       if args.tile_order != "rows" else False)
     static_times = time_schedule(spp)
     frame_no = [0]
     last = {}
