@@ -508,8 +508,9 @@ def predict_partition(args, cfg):
     W, H = cfg["W"], cfg["H"]
     spp = args.spp or cfg["spp"]
     animated = bool(cfg.get("animated"))
+    n_ctx = (args.overlap if args.overlap >= 0 else 1) + 1   # renderer contexts (as main(): --overlap)
     rs, streams = [], []
-    for _ in range(2):
+    for _ in range(n_ctx):
         r = Renderer(0, W, H)
         load_into(r, cfg, scene_for_frame(cfg, 0))
         r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
@@ -518,7 +519,7 @@ def predict_partition(args, cfg):
         r.set_stream(s_.cuda_stream)
         rs.append(r)
         streams.append(s_)
-    accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_ctx)]
     torch.cuda.synchronize()
 
     def timed(tile, rank, world, nspp):
@@ -542,7 +543,7 @@ def predict_partition(args, cfg):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / args.steps * 1e3, len(fr.tiles)
 
-    out = {"config": args.config, "width": W, "height": H, "spp": spp, "steps": args.steps, "contexts": 2,
+    out = {"config": args.config, "width": W, "height": H, "spp": spp, "steps": args.steps, "contexts": n_ctx,
            "one_gpu_ms": {}, "tiles": {}, "sample_split": {}}
     ns = [int(x) for x in args.predict.split(",") if x.strip()]
     for tile in (32, 64):
