@@ -111,6 +111,9 @@ def parse():
                          "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
                          "+97%% C1, round 3). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
+    ap.add_argument("--grid-reserve", type=int, default=-1,
+                    help="with overlapping contexts, workgroups each trace launch leaves free for the other "
+                         "context's fold (rmr_set_grid_reserve); default multi_gpu.OVERLAP_GRID_RESERVE")
     ap.add_argument("--tile-order", choices=["cost", "rows", "cost-always"], default="cost",
                     help="cost: each rank hands its costliest 32x32 tiles out first where tile costs are uneven "
                          "(a 2-sample probe of every tile's map() evaluations before the timed region, "
@@ -504,7 +507,7 @@ def predict_partition(args, cfg):
     spp / N samples): T(1) / T_split(N)."""
     import torch
     from raymarchrenderer_amd import Renderer, abi, time_schedule
-    from raymarchrenderer_amd.multi_gpu import FrameRenderer
+    from raymarchrenderer_amd.multi_gpu import OVERLAP_GRID_RESERVE, FrameRenderer
     W, H = cfg["W"], cfg["H"]
     spp = args.spp or cfg["spp"]
     animated = bool(cfg.get("animated"))
@@ -523,7 +526,8 @@ def predict_partition(args, cfg):
     torch.cuda.synchronize()
 
     def timed(tile, rank, world, nspp):
-        fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams)
+        fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams,
+                           grid_reserve=args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE)
         if args.tile_order != "rows":
             fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
         f = [0]
@@ -605,7 +609,7 @@ def main():
     elif dist_on:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     from raymarchrenderer_amd import Renderer, abi, time_schedule
-    from raymarchrenderer_amd.multi_gpu import FrameRenderer, reduce_frame
+    from raymarchrenderer_amd.multi_gpu import OVERLAP_GRID_RESERVE, FrameRenderer, reduce_frame
     animated = bool(cfg.get("animated"))
 
     # overlap: two renderer contexts on two streams; consecutive frames alternate between them, so
@@ -646,7 +650,9 @@ def main():
     n_acc = n_ctx if n_ctx > 1 else (2 if dist_on else 1)
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_acc)]
     torch.cuda.synchronize()
-    fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams)
+    reserve = args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE
+    fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams,
+                       grid_reserve=reserve)
     tiles_reordered = (fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
                        if args.tile_order != "rows" else False)
     static_times = time_schedule(spp)
@@ -807,7 +813,7 @@ def main():
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
                           "samples_per_step": W * H * spp, "tile": TILE, "tile_order": "cost" if tiles_reordered else "rows",
                           "parallelism": "tiles%d" % world,
-                          "frame_streams": n_ctx},
+                          "frame_streams": n_ctx, "grid_reserve": reserve if n_ctx > 1 else 0},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity,
                "reference_equivalent_work": work_ref}
         if dist_on:

@@ -237,6 +237,13 @@ int rmr_set_tuning(rmr_ctx* ctx, int shade_threshold, int grid_per_cu, long long
 /* (shade_threshold bits 8..15, when non-zero, set the refill threshold separately: idle lanes a
  * wave collects before it fetches new units; default (and when zero) = half the shading
  * threshold, at least 2.) */
+/* Persistent-grid reserve: the trace launch leaves `blocks` workgroups of its occupancy grid
+ * unlaunched (default 0; the grid stays >= 1 workgroup). For two contexts that alternate frames on
+ * one GPU (multi_gpu.FrameRenderer): a persistent trace kernel holds every slot it gets until its
+ * queue runs out, so the other context's running-mean fold (and the next frame's zeroing) would
+ * wait for that trace's drain, and the next trace behind them; a few free slots let them run beside
+ * it. Scheduling only: results do not depend on it. RMR_E_INVALID for blocks < 0. */
+int rmr_set_grid_reserve(rmr_ctx* ctx, int blocks);
 /* Test hook: per-sample radiance (before the running mean) of the integer rect, written as
  * out[k][y-y0][x-x0][4]; sample k is seeded with times[k]. The accumulator is left unchanged. */
 int rmr_trace_samples(rmr_ctx* ctx, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out);

@@ -114,6 +114,7 @@ struct rmr_ctx {
     int cull = RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE;   // rmr_set_culling
     int instrument = 0;   // RMR_INSTR_* (rmr_set_instrument): instrumented specialised kernels
     int grid_per_cu = 0;  // 0 = occupancy
+    int grid_reserve = 0;  // persistent grid: workgroups left free of the occupancy grid (rmr_set_grid_reserve)
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
     // 1-spp frame is 65536 units and runs 0.157 -> 0.106 ms per launch specialised (the compile,
@@ -865,7 +866,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         if (c->kernel_mode == 0 && c->grid_per_cu <= 0) {
             const uint64_t per_block = (uint64_t)((use_jit ? c->jit.block : 256) / 64) * (use_jit ? c->jit.chunk : 128);
             const uint64_t want = (P.n_units + per_block - 1) / per_block;
-            grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)full_grid, want));
+            grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, full_grid - c->grid_reserve), want));
         }
         // tuned shading batch size of the kernel that runs (measured: C2 +2% at 20; the Mandelbulb
         // and the cached BVH map -1..2%)
@@ -958,6 +959,7 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = RMR_ENV("RMR_JIT_APPROX")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_APPROX;
     if (const char* e = RMR_ENV("RMR_EYE")) if (std::atoi(e) == 0) c->cull &= ~RMR_CULL_EYE;
     if (const char* e = RMR_ENV("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
+    if (const char* e = RMR_ENV("RMR_GRID_RESERVE")) c->grid_reserve = std::max(0, std::atoi(e));
     if (const char* e = RMR_ENV("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
     if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
     *out = c;
@@ -1464,6 +1466,12 @@ int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long s
     }
     if (grid_per_cu >= 0) c->grid_per_cu = grid_per_cu;
     if (samp_budget_bytes > 0) c->samp_budget = (size_t)samp_budget_bytes;
+    return RMR_OK;
+}
+
+int rmr_set_grid_reserve(rmr_ctx* c, int blocks) {
+    if (!c || blocks < 0) return RMR_E_INVALID;
+    c->grid_reserve = blocks;
     return RMR_OK;
 }
 

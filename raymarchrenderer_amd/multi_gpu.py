@@ -14,10 +14,17 @@ With two renderer contexts on two HIP streams (`renderer=[r0, r1]`, `streams=[s0
 frames also overlap on the GPU: the persistent trace kernel of frame f ends with a drain (its last,
 longest paths run on a nearly idle chip, ~1.4 ms on C2), which frame f + 1's kernel, launched on the
 other stream, fills. Each frame's zeroing, render and reduce stay ordered on its own stream.
+A persistent trace kernel keeps every workgroup slot it gets until its queue runs out, so frame f's
+fold (a small kernel after its trace) would wait for frame f + 1's drain and hold up frame f + 2
+behind it; with two contexts each trace launch leaves OVERLAP_GRID_RESERVE workgroups free
+(rmr_set_grid_reserve) for the other context's fold and zeroing (C4 +1.7%, RM2 +3%, the 8-rank C2
+rank share +1.8%, the rest within noise: profiles/r05_grid_reserve_ab.log).
 """
 import contextlib
 
 import numpy as np
+
+OVERLAP_GRID_RESERVE = 64   # workgroups (of 1536-1792 on the C2 / C4 kernels)
 
 
 def frame_tiles(W, H, tile):
@@ -73,8 +80,13 @@ class FrameRenderer:
     one-GPU box."""
 
     def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None,
-                 reduce_at_world1=False):
+                 reduce_at_world1=False, grid_reserve=OVERLAP_GRID_RESERVE):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
+        if render_fn is None and len(self.rs) > 1 and grid_reserve is not None:
+            # overlapping contexts: each trace launch leaves a few workgroup slots free, so the other
+            # context's fold and zeroing run beside it instead of waiting for its drain (rmr.h)
+            for r in self.rs:
+                r.set_grid_reserve(grid_reserve)
         self.r, self.dist, self.render_fn = self.rs[0], dist, render_fn
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
         if len(self.accs) % len(self.rs):

@@ -165,6 +165,10 @@ class Renderer:
     def set_tuning(self, shade_threshold=0, grid_per_cu=-1, samp_budget=0):
         self._chk(self._L.rmr_set_tuning(self._ctx, int(shade_threshold), int(grid_per_cu), int(samp_budget)))
 
+    def set_grid_reserve(self, blocks):
+        """Workgroups the persistent trace launch leaves free (rmr_set_grid_reserve; scheduling only)."""
+        self._chk(self._L.rmr_set_grid_reserve(self._ctx, int(blocks)))
+
     def set_env_map(self, rgba8):
         """envTex for skyColor (used with params use_env_tex=1): (h, w, 4) uint8, row 0 = up. None clears."""
         if rgba8 is None:

@@ -557,9 +557,10 @@ def test_candidate_grid_full_frame_bitexact(monkeypatch, scene):
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene", ["cornell5.scene", "csg256.scene"])
 def test_scheduling_knobs_bitexact(scene):
-    """Shading-batch size, refill threshold and persistent grid size (rmr_set_tuning) decide only
-    which lanes run which path when: the image is bitwise the same for every setting, including the
-    per-kernel default (20-lane batches on Cornell-5, 16 on the cached BVH kernel)."""
+    """Shading-batch size, refill threshold, persistent grid size (rmr_set_tuning) and the grid
+    reserve (rmr_set_grid_reserve) decide only which lanes run which path when: the image is bitwise
+    the same for every setting, including the per-kernel default (20-lane batches on Cornell-5, 16 on
+    the cached BVH kernel)."""
     from raymarchrenderer_amd import Renderer
     W, H = 160, 96
     r = Renderer(0, 64, 64)   # own context: the settings below would outlive the test
@@ -574,6 +575,15 @@ def test_scheduling_knobs_bitexact(scene):
             r.reload()
             r.render_spp(times)
             imgs.append(r.read_accum().view(np.uint32).copy())
+        # a persistent grid of one workgroup (reserve beyond the occupancy grid), then 3 left free
+        r.set_tuning(0, 0)   # (the occupancy grid again: a fixed grid per CU ignores the reserve)
+        for reserve in (1 << 20, 3):
+            r.set_grid_reserve(reserve)
+            r.reload()
+            r.render_spp(times)
+            imgs.append(r.read_accum().view(np.uint32).copy())
+        with pytest.raises(Exception):
+            r.set_grid_reserve(-1)
     finally:
         r.close()
     for k, img in enumerate(imgs[1:], 1):
