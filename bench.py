@@ -115,11 +115,11 @@ def parse():
                     help="with overlapping contexts, workgroups each trace launch leaves free for the other "
                          "context's fold (rmr_set_grid_reserve); default multi_gpu.OVERLAP_GRID_RESERVE")
     ap.add_argument("--tile-order", choices=["cost", "rows", "cost-always"], default="cost",
-                    help="cost: each rank hands its costliest 32x32 tiles out first where tile costs are uneven "
-                         "(a 2-sample probe of every tile's map() evaluations before the timed region, "
-                         "FrameRenderer.order_tiles_by_cost: the launches' drains end on cheap tiles; C3 +2.7%%, "
-                         "the others unchanged; same image bits); rows: row-major; cost-always: cost order "
-                         "whatever the spread (experiments)")
+                    help="cost: where a rank's 32x32 tiles' costs are uneven (a 2-sample probe of every tile's map() "
+                         "evaluations), trial frames in row and cost order before the timed region decide "
+                         "(FrameRenderer.order_tiles_by_cost: costliest first, the launches' drains end on cheap "
+                         "tiles; C3 +2.7%%, RM2 kept in rows, the others under the spread; same image bits); "
+                         "rows: row-major; cost-always: cost order whatever the spread, no trial (experiments)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo + CPU oracle renderer); no GPU")
     ap.add_argument("--share-gpu", action="store_true",
@@ -653,9 +653,12 @@ def main():
     reserve = args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams,
                        grid_reserve=reserve)
-    tiles_reordered = (fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
-                       if args.tile_order != "rows" else False)
     static_times = time_schedule(spp)
+    # cost order where the tiles' costs are uneven and trial frames in both orders say it is faster
+    # (cost-always: without the trial; animated: the trial frames use frame 0's scene and seeds)
+    tiles_reordered = (fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0,
+                                              frame_times=None if args.tile_order == "cost-always" else static_times)
+                       if args.tile_order != "rows" else False)
     frame_no = [0]
     last = {}
 
@@ -812,6 +815,7 @@ def main():
                                                        "rm3": "RayMarch3.glsl"}[variant_of(cfg)], W, H, spp, BOUNCES),
                           "config": args.config, "width": W, "height": H, "spp": spp, "max_bounces": BOUNCES,
                           "samples_per_step": W * H * spp, "tile": TILE, "tile_order": "cost" if tiles_reordered else "rows",
+                          "tile_order_trial_ms": getattr(fr, "tile_order_trial_ms", None),
                           "parallelism": "tiles%d" % world,
                           "frame_streams": n_ctx, "grid_reserve": reserve if n_ctx > 1 else 0},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity,

@@ -131,27 +131,72 @@ class FrameRenderer:
         self.last = acc
         return acc
 
-    def order_tiles_by_cost(self, times, min_spread=3.0):
-        """Hand this rank's costliest tiles out first where tile costs are uneven. The work queue
+    def order_tiles_by_cost(self, times, min_spread=3.0, frame_times=None, trials=4):
+        """Hand this rank's costliest tiles out first where that makes frames faster. The work queue
         gives units out in tile-list order within each sample, so a launch ends (drains) on its last
         tiles' paths; with the cheap ones last (by each tile's map() evaluations in a probe over
-        `times`, tile_costs) the drain is shorter. Measured (r05_tile_order_bench.log): the Mandelbulb
-        (tile costs up to 5x the mean) +2.7%, Cornell-5 / C5 / RM3 (under 2x) within noise, so the order
-        changes only when the costliest tile exceeds `min_spread` x the mean. Each pixel's samples are
-        the same whatever the order, so the image is the same bits. Call before the first frame (the
-        probe writes the first accumulator, which every frame zeroes). Returns whether it reordered."""
-        if self.render_fn is not None or not len(self.tiles):
+        `times`, tile_costs) the drain is shorter. Only where the costliest tile exceeds `min_spread` x
+        the mean is the order tried; then, with `frame_times`, `trials` frames in each order (twice,
+        interleaved, after a frame per context in that order, before the caller's frames; every rank
+        the same frames, the timings summed over ranks) decide. Measured (r05_tile_order_bench.log, r05_tile_order_rm2.log): the Mandelbulb
+        (tile costs up to 5x the mean) +2.7%, the RM2 NEE frame (sky tiles) -11%, Cornell-5 / C5 / RM3
+        (under 2x) within noise. Each pixel's samples are the same whatever the order, so the image is
+        the same bits. Call before the first frame (the probe writes the first accumulator, which every
+        frame zeroes). Returns whether it reordered."""
+        if self.render_fn is not None:
             return False
-        acc = self.accs[0]
-        with self._on_stream(0):
-            self.r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
-            cost = tile_costs(self.r, self.tiles, self.tile, times)
-            acc.zero_()
-        self.tile_cost_spread = float(cost.max() / max(1.0, cost.mean()))
-        if self.tile_cost_spread <= min_spread:
+        cost = np.zeros(0, np.int64)
+        if len(self.tiles):
+            acc = self.accs[0]
+            with self._on_stream(0):
+                self.r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
+                cost = tile_costs(self.r, self.tiles, self.tile, times)
+                acc.zero_()
+        self.tile_cost_spread = float(cost.max() / max(1.0, cost.mean())) if len(cost) else 0.0
+        trial = frame_times is not None and trials > 0
+        go = self.tile_cost_spread > min_spread
+        if trial:   # every rank runs the same trial frames (their reduces are collectives) or none
+            go = self._sum_over_ranks([float(go)])[0] > 0
+        if not go:
             return False
-        self.tiles = self.tiles[np.argsort(-cost, kind="stable")]
+        rows, by_cost = self.tiles, self.tiles[np.argsort(-cost, kind="stable")]
+        if trial:
+            t = [0.0, 0.0]
+            for _ in range(2):
+                for k, order in enumerate((rows, by_cost)):
+                    self.tiles = order
+                    # untimed: one frame per context (its tile-list upload after the switch)
+                    self._time_frames(frame_times, len(self.rs))
+                    t[k] += self._time_frames(frame_times, trials)
+            t = self._sum_over_ranks(t)
+            self.tile_order_trial_ms = [round(x / (2 * trials) * 1e3, 4) for x in t]
+            if t[1] >= t[0]:
+                self.tiles = rows
+                return False
+        self.tiles = by_cost
         return True
+
+    def _time_frames(self, times, n):
+        import time
+
+        import torch
+        self.finish()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            self.frame(times)
+        self.finish()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    def _sum_over_ranks(self, vals):
+        if not _multi(self.dist):
+            return vals
+        import torch
+        dev = self.accs[0].device
+        x = torch.tensor(vals, dtype=torch.float64, device=dev if dev.type == "cuda" and self.dist.get_backend() == "nccl" else "cpu")
+        self.dist.all_reduce(x)
+        return x.cpu().tolist()
 
     def next_renderer(self):
         """The renderer context the next frame() uses (e.g. to load that frame's scene)."""
