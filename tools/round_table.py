@@ -2,7 +2,9 @@
 profiles/<TAG>_bench_<cfg>.json (bench.py lines, tools/gpu_benchall.sh) and profiles/<TAG>_<cfg>_pmc.json
 (tools/round_profiles.sh + summarize_profile.py).
 
-    python tools/round_table.py r05z
+    python tools/round_table.py r05z [PMC_FALLBACK_TAG]
+(a config without a PMC profile under TAG takes PMC_FALLBACK_TAG's, marked with *: same kernels, an
+earlier profile)
 """
 import json
 import os
@@ -20,18 +22,21 @@ def load(name):
     return json.load(open(p)) if os.path.exists(p) else None
 
 
-def main(tag):
+def main(tag, fallback=None):
     print("| config | Msamples/s | ms per step | kernel ms per launch: bench / rocprof | roofline frac (executed flops) "
           "| HBM per launch (PMC) | VALU lane util | wait on memory | CPU leg: Msamples/s (threads), per core | PSNR vs reference |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for cfg, name in ROWS:
         b = load("%s_bench_%s.json" % (tag, cfg))
         m = load("%s_%s_pmc.json" % (tag, cfg))
+        star = ""
+        if m is None and fallback:
+            m, star = load("%s_%s_pmc.json" % (fallback, cfg)), "*"
         if b is None:
             continue
         r, c, ps = b["roofline"], b.get("cpu_baseline") or {}, b.get("psnr_vs_reference") or {}
         d = (m or {}).get("derived", {})
-        rp = "%.3f" % ((m or {}).get("k_trace_avg_ns", 0) / 1e6) if m else "—"
+        rp = ("%.3f" % ((m or {}).get("k_trace_avg_ns", 0) / 1e6) + star) if m else "—"
         hbm = d.get("hbm_bytes")
         hbm_s = ("%.2f GB" % (hbm / 1e9)) if hbm and hbm >= 1e8 else (("%.1f MB" % (hbm / 1e6)) if hbm else "—")
         cpu = ("%.3g (%d), %.3g" % (c["value"], c["cores"], c.get("per_core", c["value"] / c["cores"]))) if c else "—"
@@ -43,4 +48,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r05z")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r05z", sys.argv[2] if len(sys.argv) > 2 else None)
