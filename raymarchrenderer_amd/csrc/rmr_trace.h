@@ -1403,6 +1403,22 @@ RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
     return normalize(vmix(top, bot, posy + j3 / H));
 }
 
+// a finished sample's plane store: write-once data the fold reads once, stored nontemporal (streamed
+// past the L2 instead of occupying it): RM2 +15%, the other classes within noise; the fold's loads
+// nontemporal as well measured neutral (r05_nt_planes_ab.log)
+#ifndef RMR_NT_PLANES
+#define RMR_NT_PLANES 1   // (0: plain stores, A/B)
+#endif
+RMR_D void store_sample(float4* p, float4 v) {
+#if RMR_NT_PLANES
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (f4v*)p);
+#else
+    *p = v;
+#endif
+}
+
 // End of trace(): store the channel result into the sample plane. Returns true when the sample
 // is complete; otherwise (separateChannels, RM1:586-598) the lane is parked in PH_RESTART and the
 // next channel's trace starts where new units start (one inlined copy of the ray setup).
@@ -1432,14 +1448,14 @@ RMR_D bool finish_trace(const KParams& P, Lane& L) {
             else if (wl < 420.0f) alpha = div_k(wl - 380.0f, 40.0f);
             else alpha = 1.0f;
             const V3 c = (v3(R, G, B) * alpha) * L.power;
-            P.samp[L.unit] = make_float4(c.x, c.y, c.z, 1.0f);
+            store_sample(P.samp + L.unit, make_float4(c.x, c.y, c.z, 1.0f));
             return true;
         }
         if (L.chan < 0) {
 #ifdef RMR_DIAG_NO_STORE   // timing experiment only (wrong planes): what the plane stores cost
             if (res.x == -1234.5f)
 #endif
-            P.samp[L.unit] = make_float4(res.x, res.y, res.z, 1.0f);
+            store_sample(P.samp + L.unit, make_float4(res.x, res.y, res.z, 1.0f));
             return true;
         }
         // separateChannels: (r + g) + b, RM1:597; the partial sum lives in the sample plane
