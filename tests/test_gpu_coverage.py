@@ -308,3 +308,35 @@ def test_frame_renderer_cost_ordered_tiles_same_frame(scene):
     finally:
         r.close()
         ref.close()
+
+
+def test_frame_renderer_tile_order_trial_same_frame():
+    """order_tiles_by_cost with trial frames (bench.py's default): two overlapping contexts render
+    frames in row and cost order, the faster order is kept, and the next frame is the row-major frame
+    bit for bit whichever it is."""
+    import torch
+    from raymarchrenderer_amd import Renderer
+    from raymarchrenderer_amd.multi_gpu import FrameRenderer, frame_tiles
+    W, H, tile = 192, 128, 32
+    path = os.path.join(SCENES, "mandelbulb.scene")
+    rs = [Renderer(0, W, H) for _ in range(2)]
+    ref = Renderer(0, W, H)
+    try:
+        for x in rs + [ref]:
+            _setup(x, path, W, H, max_bounces=2)
+        accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+        fr = FrameRenderer(rs, accs, W, H, tile, 0, 1)
+        times = time_schedule(4, frame=3)
+        fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0, frame_times=times, trials=2)
+        assert len(fr.tile_order_trial_ms) == 2 and min(fr.tile_order_trial_ms) > 0
+        rows = np.array(frame_tiles(W, H, tile), np.int32)
+        assert sorted(map(tuple, fr.tiles.tolist())) == sorted(map(tuple, rows.tolist()))
+        out = fr.frame(times)
+        fr.finish()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().copy()
+        ref.render_tiles(times, rows, tile)
+        assert _same(got, ref.read_accum()).all()
+    finally:
+        for x in rs + [ref]:
+            x.close()
