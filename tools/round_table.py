@@ -2,9 +2,8 @@
 profiles/<TAG>_bench_<cfg>.json (bench.py lines, tools/gpu_benchall.sh) and profiles/<TAG>_<cfg>_pmc.json
 (tools/round_profiles.sh + summarize_profile.py).
 
-    python tools/round_table.py r05z [PMC_FALLBACK_TAG]
-(a config without a PMC profile under TAG takes PMC_FALLBACK_TAG's, marked with *: same kernels, an
-earlier profile)
+    python tools/round_table.py r05z [PMC_TAG ...]
+(a config without a PMC profile under TAG takes the first of the PMC_TAGs that has one, marked with *)
 """
 import json
 import os
@@ -22,7 +21,7 @@ def load(name):
     return json.load(open(p)) if os.path.exists(p) else None
 
 
-def main(tag, fallback=None):
+def main(tag, fallbacks=()):
     print("| config | Msamples/s | ms per step | kernel ms per launch: bench / rocprof | roofline frac (executed flops) "
           "| HBM per launch (PMC) | VALU lane util | wait on memory | CPU leg: Msamples/s (threads), per core | PSNR vs reference |")
     print("|---|---|---|---|---|---|---|---|---|---|")
@@ -30,8 +29,10 @@ def main(tag, fallback=None):
         b = load("%s_bench_%s.json" % (tag, cfg))
         m = load("%s_%s_pmc.json" % (tag, cfg))
         star = ""
-        if m is None and fallback:
-            m, star = load("%s_%s_pmc.json" % (fallback, cfg)), "*"
+        for fb in fallbacks:
+            if m is not None:
+                break
+            m, star = load("%s_%s_pmc.json" % (fb, cfg)), "*"
         if b is None:
             continue
         r, c, ps = b["roofline"], b.get("cpu_baseline") or {}, b.get("psnr_vs_reference") or {}
@@ -48,4 +49,4 @@ def main(tag, fallback=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r05z", sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1] if len(sys.argv) > 1 else "r05z", sys.argv[2:])
