@@ -1403,11 +1403,12 @@ RMR_D V3 primary_dir(const KParams& P, int px, int py, float time, float& rc) {
     return normalize(vmix(top, bot, posy + j3 / H));
 }
 
-// a finished sample's plane store: write-once data the fold reads once, stored nontemporal (streamed
-// past the L2 instead of occupying it): RM2 +15%, the other classes within noise; the fold's loads
-// nontemporal as well measured neutral (r05_nt_planes_ab.log)
+// a finished sample's plane store: write-once data the fold reads once. Nontemporal (streamed past the
+// L2) where the hipRTC source asks for it (rmr_jit.cpp: RM2 +15%, C4's HBM traffic -37%; the L2 merges
+// the lines' 16-B pieces better for the other classes); the fold's loads nontemporal measured neutral
+// (r05_nt_planes_ab.log)
 #ifndef RMR_NT_PLANES
-#define RMR_NT_PLANES 1   // (0: plain stores, A/B)
+#define RMR_NT_PLANES 0
 #endif
 RMR_D void store_sample(float4* p, float4 v) {
 #if RMR_NT_PLANES
