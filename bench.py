@@ -133,6 +133,17 @@ def parse():
                          "speed-up (SURVEY §8e)")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip rank 0's check of the last reduced frame against a one-context render")
+    ap.add_argument("--api", choices=["frame", "render", "group"], default="frame",
+                    help="frame: the batched frame path (rmr_render_tiles, the headline); render: the reference's "
+                         "own call pattern through the drop-in, Program.cpp:232-284's fixed-spp loop: a 4x4 tile "
+                         "grid in spiral order, every tile's samples one rmr_render (Graphics::Render) call each, "
+                         "no sync per call; one step = one frame (a separate line, not the headline); group: the "
+                         "C++ host's single-process device group (librmr_group.so: --gpus N devices from ONE "
+                         "process, ncclCommInitAll, one RCCL reduce per frame; not under a launcher)")
+    ap.add_argument("--grid", default="4x4", help="--api render: the tile grid (Program.cpp:106-107)")
+    ap.add_argument("--call-batching", type=int, default=-1, choices=[-1, 0, 1],
+                    help="--api render: rmr_set_call_batching (-1 auto = on for a context that owns its stream, "
+                         "the default; 0: one launch per call)")
     return ap.parse_args()
 
 
@@ -507,7 +518,7 @@ def predict_partition(args, cfg):
     spp / N samples): T(1) / T_split(N)."""
     import torch
     from raymarchrenderer_amd import Renderer, abi, time_schedule
-    from raymarchrenderer_amd.multi_gpu import OVERLAP_GRID_RESERVE, FrameRenderer
+    from raymarchrenderer_amd.multi_gpu import OVERLAP_GRID_RESERVE, FrameRenderer, frame_tile_costs
     W, H = cfg["W"], cfg["H"]
     spp = args.spp or cfg["spp"]
     animated = bool(cfg.get("animated"))
@@ -524,12 +535,21 @@ def predict_partition(args, cfg):
         streams.append(s_)
     accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(n_ctx)]
     torch.cuda.synchronize()
+    cost_maps = {}   # per tile size: every tile's probe cost, probed once and sliced per rank share
 
     def timed(tile, rank, world, nspp):
         fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams,
                            grid_reserve=args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE)
         if args.tile_order != "rows":
-            fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0)
+            if tile not in cost_maps:
+                with torch.cuda.stream(streams[0]):
+                    rs[0].bind_accum(accs[0].data_ptr(), accs[0].numel() * accs[0].element_size())
+                    cost_maps[tile] = frame_tile_costs(rs[0], W, H, tile, time_schedule(2))
+                    accs[0].zero_()
+            # as main(): trial frames in both orders decide (cost-always: no trial), here per rank share
+            fr.order_tiles_by_cost(time_schedule(2), min_spread=0.0 if args.tile_order == "cost-always" else 3.0,
+                                   frame_times=None if args.tile_order == "cost-always" else time_schedule(nspp),
+                                   cost_map=cost_maps[tile])
         f = [0]
 
         def step():
@@ -545,7 +565,9 @@ def predict_partition(args, cfg):
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / args.steps * 1e3, len(fr.tiles)
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        fr.close()
+        return ms, len(fr.tiles)
 
     out = {"config": args.config, "width": W, "height": H, "spp": spp, "steps": args.steps, "contexts": n_ctx,
            "one_gpu_ms": {}, "tiles": {}, "sample_split": {}}
@@ -577,9 +599,158 @@ def predict_partition(args, cfg):
     return 0
 
 
+def api_render_bench(args, cfg):
+    """--api render: the drop-in under the caller it exists for. Program.cpp:232-284 (fixed spp): for
+    each tile of a 4x4 grid in spiral order, `spp` calls of Graphics::Render(time, min, max,
+    currentSample), one sample each (G.cpp:314-354 -> rmr_render), no sync between calls. One step = one
+    frame (Reload's zeroing, then every call). Reports Msamples/s, calls/s and where a call's time goes:
+    the trace and fold kernels (HIP events around each launch) and the rest, the GPU idle between
+    launches (host dispatch, copies, launch latency). Checks the frame bit for bit against one batched
+    rmr_render_spp of the whole frame (same seeds): the per-call path computes the same samples."""
+    import numpy as np
+    import torch
+    from raymarchrenderer_amd import Renderer, abi, tile_spiral, time_schedule
+    W, H = cfg["W"], cfg["H"]
+    spp = args.spp or cfg["spp"]
+    gw, gh = (int(v) for v in args.grid.lower().split("x"))
+    cw, ch = W // gw, H // gh   # Program.cpp:108-109 (a remainder is not rendered)
+    order = tile_spiral(gw, gh)   # Program.cpp:113-115, 203-222
+    times = time_schedule(spp)
+    tl = [float(t) for t in times]
+    r = Renderer(0, W, H)
+    load_into(r, cfg, scene_for_frame(cfg, 0))
+    r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
+    r.set_call_batching(args.call_batching)
+    rects = [((x * cw, y * ch), ((x + 1) * cw, (y + 1) * ch)) for x, y in order]
+
+    def frame():
+        r.reload()   # Program.cpp:172 (Graphics::Reload at the render's start: the accumulator zeroed)
+        for mn, mx in rects:
+            for s in range(spp):
+                r.render(tl[s], mn, mx, s)
+
+    for _ in range(max(1, args.warmup)):
+        frame()
+    r.sync()
+    r.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    host = 0.0
+    for _ in range(args.steps):
+        h0 = time.perf_counter()
+        frame()
+        host += time.perf_counter() - h0
+        r.sync()
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+    got = r.read_accum()
+    calls = len(rects) * spp * args.steps
+    samples = float(cw * ch * len(rects)) * spp * args.steps
+    # the same frame as one batched call (checked bit for bit, then timed the same number of times)
+    r.reload()
+    r.render_spp(times, rect=(0, 0, cw * gw, ch * gh))
+    want = r.read_accum()
+    same = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    r.sync()
+    tb = time.perf_counter()
+    for _ in range(args.steps):
+        r.reload()
+        r.render_spp(times, rect=(0, 0, cw * gw, ch * gh))
+    r.sync()
+    batched = samples / (time.perf_counter() - tb) / 1e6
+    r.close()
+    ms_step = elapsed / args.steps * 1e3
+    out = {"metric": METRIC, "value": round(samples / elapsed / 1e6, 2), "unit": "Msamples/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": "%s %dx%d %d spp %d bounces through rmr_render, one call per tile and sample "
+                                  "(Program.cpp fixed-spp loop)" % (cfg["name"], W, H, spp, cfg["bounces"]),
+                      "config": args.config, "api": "render", "grid": "%dx%d" % (gw, gh), "tile_px": [cw, ch],
+                      "order": "spiral (Program.cpp:203-222)", "call_batching": args.call_batching,
+                      "width": W, "height": H, "spp": spp,
+                      "max_bounces": cfg["bounces"]},
+           "calls": {"per_step": len(rects) * spp, "per_s": round(calls / elapsed, 1),
+                     "us_per_call": round(elapsed / calls * 1e6, 3),
+                     "host_us_per_call": round(host / calls * 1e6, 3),
+                     "trace_us_per_call": round(st.trace_ms / calls * 1e3, 3),
+                     "fold_us_per_call": round(st.fold_ms / calls * 1e3, 3),
+                     "gap_us_per_call": round((elapsed * 1e3 - st.trace_ms - st.fold_ms) / calls * 1e3, 3),
+                     "jit_launches": int(st.jit_launches), "trace_launches": int(st.trace_launches),
+                     "note": "gap = wall time minus the summed trace and fold kernel times (HIP events), per call: "
+                             "the GPU idle between one call's kernels and the next's (with call batching a launch "
+                             "serves many calls: trace_launches < calls)"},
+           "batched_same_frame_msamples_per_s": round(batched, 2),
+           "bitwise_equal_to_batched": same}
+    print(json.dumps(out), flush=True)
+    return 0 if same else 1
+
+
+def api_group_bench(args, cfg):
+    """--api group: the frame through librmr_group.so (include/rmr_group.h), the multi-GPU path of the C++
+    host: --gpus N devices driven from this one process, the frame's 32x32 tiles dealt round-robin, two
+    contexts per device, one ncclReduce per frame. Same workload, seeds and step as the headline; the
+    last frame is checked bit for bit against one context's render of the whole frame."""
+    import numpy as np
+    from raymarchrenderer_amd import Renderer, abi, time_schedule
+    from raymarchrenderer_amd.group import DeviceGroup
+    W, H = cfg["W"], cfg["H"]
+    spp = args.spp or cfg["spp"]
+    if cfg.get("animated"):
+        sys.exit("bench.py --api group: static configs only")
+    scene = scene_for_frame(cfg, 0)
+    prm = abi.default_params(max_bounces=cfg["bounces"])
+    g = DeviceGroup(list(range(args.gpus)), W, H, tile=TILE)
+    if scene is None:
+        g.load_builtin(variant_of(cfg))
+    else:
+        g.load_scene(scene, variant_of(cfg))
+    g.set_params(prm)
+    g.reload()
+    times = time_schedule(spp)
+    for _ in range(max(1, args.warmup)):
+        g.render_frame(times)
+    g.sync()
+    g.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.render_frame(times)
+    g.sync()
+    elapsed = time.perf_counter() - t0
+    per = [g.stats(m) for m in range(g.size())]
+    got = g.read_frame()
+    g.close()
+    r = Renderer(0, W, H)
+    load_into(r, cfg, scene)
+    r.set_params(prm)
+    r.render_spp(times)
+    same = bool(np.array_equal(got.view(np.uint32), r.read_accum().view(np.uint32)))
+    r.close()
+    samples = float(W) * H * spp * args.steps
+    out = {"metric": METRIC, "value": round(samples / elapsed / 1e6, 2), "unit": "Msamples/s", "n_gpus": args.gpus,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": "%s %dx%d %d spp %d bounces through the single-process device group (librmr_group.so)"
+                                  % (cfg["name"], W, H, spp, cfg["bounces"]), "config": args.config, "api": "group",
+                      "width": W, "height": H, "spp": spp, "max_bounces": cfg["bounces"], "tile": TILE,
+                      "parallelism": "tiles%d (one process, ncclCommInitAll)" % args.gpus},
+           "members": [{"device": m, "trace_ms_per_step": round(s.trace_ms / args.steps, 3),
+                        "trace_launches": int(s.trace_launches), "map_evals": int(s.map_evals)} for m, s in enumerate(per)],
+           "bitwise_equal_to_one_context": same}
+    print(json.dumps(out), flush=True)
+    return 0 if same else 1
+
+
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
+    if args.api == "group":
+        if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            sys.exit("bench.py --api group drives every GPU from one process (no launcher)")
+        sys.exit(api_group_bench(args, cfg))
+    if args.api == "render":
+        if args.gpus != 1 or "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            sys.exit("bench.py --api render runs on one GPU (the reference's single context)")
+        sys.exit(api_render_bench(args, cfg))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))

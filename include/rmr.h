@@ -122,6 +122,20 @@ int rmr_reload(rmr_ctx* ctx);
  * overwrites). `time` is the rand() seed uniform. */
 int rmr_render(rmr_ctx* ctx, float time, float min_x, float min_y, float max_x, float max_y,
                uint32_t current_sample);
+/* Call batching of rmr_render (the reference calls Graphics::Render once per tile and sample,
+ * Program.cpp:232-284; one such launch renders one sample of a tile and is bound by its longest path,
+ * not by the chip). With batching on, rmr_render records the call (checking its state errors at once)
+ * and launches nothing; consecutive samples of a rect, and rects holding the same samples, go out
+ * together as one launch when any other entry point is called (rmr_sync, rmr_read_accum, rmr_save_bmp,
+ * rmr_display, a setter, ...; rmr_accum_device_ptr included), when an overlapping rect or a
+ * non-consecutive sample of a held rect arrives, or when 2^28 units are held. Bitwise equal to
+ * unbatched calls (each pixel's samples, their seeds and their running-mean order are the same). Like
+ * GL, which also queues the reference's dispatches until something reads their results, the work
+ * starts at the next flush: a caller that orders its own stream work on the context's accumulator
+ * without calling into rmr must flush first (rmr_sync). mode 1 on, 0 off, -1 auto (default): on while
+ * the context owns its stream and its accumulator (no rmr_set_stream / rmr_bind_accum), since only
+ * then are all readers inside rmr. rmr_destroy drops calls still held. */
+int rmr_set_call_batching(rmr_ctx* ctx, int mode);
 /* Batched fast path: samples first_sample .. first_sample+nspp-1 of every pixel in the integer
  * rect [x0,x1)x[y0,y1), sample k seeded with times[k]. Bitwise equal to nspp rmr_render calls
  * with the same times. */

@@ -91,11 +91,27 @@ struct rmr_ctx {
     bool accum_external = false;
     float4* d_samp = nullptr;
     size_t samp_cap = 0;
-    TileXY* d_tiles = nullptr;
-    size_t tiles_cap = 0;
-    std::vector<TileXY> tiles_host;
+    // device tile lists by content (tile_list): a list is uploaded once and reused by every later launch
+    // with the same tiles (the reference's per-tile, per-sample calls; a rank's share each frame) with no
+    // copy and no stream sync; least recently used entries go beyond kTileCacheEntries
+    struct TileList { std::vector<TileXY> host; TileXY* dev; uint64_t hash; uint64_t used; };
+    std::vector<TileList> tile_cache;
+    uint64_t tile_clock = 0;
+    // seeds of launches of more than one sample: a pinned host ring and its device twin, so the copy is
+    // asynchronous (from the caller's pageable array hipMemcpyAsync had waited for the copy, i.e. for the
+    // work queued before it); a one-sample launch passes its seed as a kernel argument (KParams::time1)
     float* d_times = nullptr;
-    size_t times_cap = 0;
+    float* h_times = nullptr;
+    size_t times_cap = 0, times_pos = 0;
+    bool queue_dirty = false;   // a trace launch went out without the fold that zeroes the queue after it
+    // deferred one-sample calls (rmr_render, the reference's Graphics::Render pattern): per pixel rect
+    // the consecutive samples requested so far, launched together at the next call of any other entry
+    // point (flush_calls); rmr_set_call_batching: -1 auto (on while the context owns its stream and its
+    // accumulator), 0 off, 1 on
+    struct Deferred { int x0, y0, x1, y1; uint32_t s0; std::vector<float> times; };
+    std::vector<Deferred> deferred;
+    uint64_t deferred_units = 0;
+    int call_batching = -1;
     unsigned long long* d_queue = nullptr;
     unsigned long long* d_counters = nullptr;
     // timing
@@ -658,19 +674,71 @@ int ensure_samp(rmr_ctx* c, size_t n) {
     return RMR_OK;
 }
 
-int set_tiles(rmr_ctx* c, const std::vector<TileXY>& t) {
-    if (t.size() == c->tiles_host.size() && std::equal(t.begin(), t.end(), c->tiles_host.begin(),
-                                                      [](const TileXY& a, const TileXY& b) { return a.x == b.x && a.y == b.y; }))
-        return RMR_OK;
-    if (t.size() > c->tiles_cap) {
-        if (c->d_tiles) (void)hipFree(c->d_tiles);
-        c->d_tiles = nullptr;
-        HIPCHK(c, hipMalloc((void**)&c->d_tiles, std::max<size_t>(1, t.size()) * sizeof(TileXY)));
-        c->tiles_cap = t.size();
+constexpr size_t kTileCacheEntries = 64;
+
+uint64_t tiles_hash(const std::vector<TileXY>& t) {
+    uint64_t h = 1469598103934665603ull ^ t.size();
+    for (const TileXY& v : t) {
+        h = (h ^ (uint32_t)v.x) * 1099511628211ull;
+        h = (h ^ (uint32_t)v.y) * 1099511628211ull;
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(c->d_tiles, t.data(), t.size() * sizeof(TileXY), hipMemcpyHostToDevice));
-    c->tiles_host = t;
+    return h;
+}
+
+// The device copy of a tile list (cached by content, see rmr_ctx::tile_cache).
+int tile_list(rmr_ctx* c, const std::vector<TileXY>& t, const TileXY** out) {
+    const uint64_t h = tiles_hash(t);
+    auto same = [](const TileXY& a, const TileXY& b) { return a.x == b.x && a.y == b.y; };
+    for (auto& e : c->tile_cache)
+        if (e.hash == h && e.host.size() == t.size() && std::equal(t.begin(), t.end(), e.host.begin(), same)) {
+            e.used = ++c->tile_clock;
+            *out = e.dev;
+            return RMR_OK;
+        }
+    if (c->tile_cache.size() >= kTileCacheEntries) {
+        auto lru = std::min_element(c->tile_cache.begin(), c->tile_cache.end(),
+                                    [](const rmr_ctx::TileList& a, const rmr_ctx::TileList& b) { return a.used < b.used; });
+        HIPCHK(c, hipStreamSynchronize(c->stream));   // launches queued before may still read it
+        (void)hipFree(lru->dev);
+        c->tile_cache.erase(lru);
+    }
+    rmr_ctx::TileList e{t, nullptr, h, ++c->tile_clock};
+    HIPCHK(c, hipMalloc((void**)&e.dev, std::max<size_t>(1, t.size()) * sizeof(TileXY)));
+    // a new buffer no queued launch reads: a plain synchronous copy, no wait for the stream
+    const hipError_t er = hipMemcpy(e.dev, t.data(), t.size() * sizeof(TileXY), hipMemcpyHostToDevice);
+    if (er != hipSuccess) {
+        (void)hipFree(e.dev);
+        return fail(c, RMR_E_HIP, std::string("tile list upload: ") + hipGetErrorString(er));
+    }
+    c->tile_cache.push_back(std::move(e));
+    *out = c->tile_cache.back().dev;
+    return RMR_OK;
+}
+
+// The launch's seeds on the device (launches of more than one sample; see rmr_ctx::h_times).
+int stage_times(rmr_ctx* c, const float* times, uint32_t n, const float** out) {
+    if (n > c->times_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->d_times) (void)hipFree(c->d_times);
+        if (c->h_times) (void)hipHostFree(c->h_times);
+        c->d_times = nullptr;
+        c->h_times = nullptr;
+        c->times_cap = c->times_pos = 0;
+        const size_t cap = std::max<size_t>(n, (size_t)1 << 16);
+        HIPCHK(c, hipMalloc((void**)&c->d_times, cap * sizeof(float)));
+        HIPCHK(c, hipHostMalloc((void**)&c->h_times, cap * sizeof(float), hipHostMallocDefault));
+        c->times_cap = cap;
+    }
+    if (c->times_pos + n > c->times_cap) {   // wrap: every copy and launch that used the ring is done
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->times_pos = 0;
+    }
+    float* h = c->h_times + c->times_pos;
+    float* d = c->d_times + c->times_pos;
+    std::memcpy(h, times, n * sizeof(float));
+    HIPCHK(c, hipMemcpyAsync(d, h, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    c->times_pos += n;
+    *out = d;
     return RMR_OK;
 }
 
@@ -739,20 +807,16 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     if (tiles.empty() || nspp == 0) return RMR_OK;
     if (!c->view_set) default_view(c);
     int r;
-    if ((r = set_tiles(c, tiles))) return r;
+    const TileXY* d_tiles = nullptr;
+    if ((r = tile_list(c, tiles, &d_tiles))) return r;
     const size_t plane = tiles.size() * 64;
     size_t chunk = std::max<size_t>(1, c->samp_budget / (plane * sizeof(float4)));
     chunk = std::min<size_t>(chunk, nspp);
     // the trace kernel indexes units with 32 bits (atomic work counter included): < 2^31 per launch
     chunk = std::max<size_t>(1, std::min<size_t>(chunk, ((size_t)1 << 31) / plane));
     if ((r = ensure_samp(c, plane * chunk))) return r;
-    if (nspp > c->times_cap) {
-        if (c->d_times) (void)hipFree(c->d_times);
-        c->d_times = nullptr;
-        HIPCHK(c, hipMalloc((void**)&c->d_times, nspp * sizeof(float)));
-        c->times_cap = nspp;
-    }
-    HIPCHK(c, hipMemcpyAsync(c->d_times, times, nspp * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    const float* d_times = nullptr;
+    if (nspp > 1 && (r = stage_times(c, times, nspp, &d_times))) return r;
 
     const CompiledScene& s = c->scene;
     KParams P{};
@@ -825,7 +889,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     P.env_wf[2] = (float)(c->env_w - 1); P.env_wf[3] = (float)(c->env_h - 1);
     P.eye_xy = P.eye[0] + P.eye[1];
     P.x0 = x0; P.y0 = y0; P.x1 = x1; P.y1 = y1;
-    P.tiles = c->d_tiles;
+    P.tiles = d_tiles;
     P.n_tiles = (int)tiles.size();
     P.samp = c->d_samp;
     P.accum = c->d_accum;
@@ -856,7 +920,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         const uint32_t n = (uint32_t)std::min<size_t>(chunk, nspp - k0);
         P.nspp = n;
         P.first_sample = first_sample + k0;
-        P.times = c->d_times + k0;
+        P.times = d_times ? d_times + k0 : nullptr;
+        P.time1 = times[k0];   // the seed when this launch has one sample (unit_pixel)
         P.n_units = (uint64_t)n * plane;
         // a persistent grid no larger than the launch's work: one work chunk per wave at most (a
         // 256x256 1-spp launch (C1) on the full grid: 0.47 ms, almost all of it waves that find no
@@ -874,7 +939,8 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
             P.shade_threshold = use_jit ? c->jit.shade_t : 16;
             P.refill_threshold = refill_for(c->refill_threshold, P.shade_threshold);
         }
-        HIPCHK(c, hipMemsetAsync(c->d_queue, 0, rmr::kQueueBytes, c->stream));
+        if (c->queue_dirty) HIPCHK(c, hipMemsetAsync(c->d_queue, 0, rmr::kQueueBytes, c->stream));
+        c->queue_dirty = true;   // until the fold that zeroes it is queued
         EventPair ev = get_events(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
         if (use_jit) {
@@ -887,6 +953,7 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         }
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         HIPCHK(c, rmr::launch_fold(P, c->stream));
+        c->queue_dirty = false;
         HIPCHK(c, hipEventRecord(ev.c, c->stream));
         c->pending.push_back(ev);
         c->stats.trace_launches++;
@@ -904,7 +971,68 @@ std::vector<TileXY> rect_tiles(int x0, int y0, int x1, int y1) {
 
 int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+bool batching_on(const rmr_ctx* c) {
+    return c->call_batching > 0 || (c->call_batching < 0 && c->own_stream && !c->accum_external);
+}
+
+// deferred units beyond which rmr_render launches what it holds (2^28 units: 4 GiB of sample planes)
+constexpr uint64_t kDeferredUnitsMax = (uint64_t)1 << 28;
+constexpr size_t kDeferredRectsMax = 4096;
+
+// Launch the deferred one-sample calls. Rects holding the same samples (same first index, same seeds)
+// whose union is a rectangle go out as one launch over that rectangle (the reference's 4x4 grid, fixed
+// or progressive: the whole grid in one launch); any other rect goes out as a launch of its own (a
+// launch clips to one rect: a tile of a rect whose edge is off the 8-pixel grid reaches into its
+// neighbour). Bitwise equal to the calls made one by one: each pixel gets the same samples with the same
+// seeds in the same order, and the held rects are disjoint (rmr_render flushes before an overlapping
+// call).
+int flush_calls(rmr_ctx* c) {
+    if (c->deferred.empty()) return RMR_OK;
+    std::vector<rmr_ctx::Deferred> d;
+    d.swap(c->deferred);
+    c->deferred_units = 0;
+    std::vector<char> done(d.size(), 0);
+    for (size_t i = 0; i < d.size(); i++) {
+        if (done[i]) continue;
+        std::vector<size_t> grp;
+        int bx0 = d[i].x0, by0 = d[i].y0, bx1 = d[i].x1, by1 = d[i].y1;
+        uint64_t area = 0;
+        for (size_t j = i; j < d.size(); j++) {
+            if (done[j] || d[j].s0 != d[i].s0 || d[j].times.size() != d[i].times.size() ||
+                std::memcmp(d[j].times.data(), d[i].times.data(), d[i].times.size() * sizeof(float)) != 0)
+                continue;
+            grp.push_back(j);
+            done[j] = 1;
+            bx0 = std::min(bx0, d[j].x0); by0 = std::min(by0, d[j].y0);
+            bx1 = std::max(bx1, d[j].x1); by1 = std::max(by1, d[j].y1);
+            area += (uint64_t)(d[j].x1 - d[j].x0) * (uint64_t)(d[j].y1 - d[j].y0);
+        }
+        const uint32_t n = (uint32_t)d[i].times.size();
+        if (area == (uint64_t)(bx1 - bx0) * (uint64_t)(by1 - by0)) {   // disjoint rects filling their box
+            const int r = render_tiles(c, rect_tiles(bx0, by0, bx1, by1), bx0, by0, bx1, by1, d[i].times.data(), d[i].s0, n);
+            if (r) return r;
+            continue;
+        }
+        for (size_t j : grp) {
+            const int r = render_tiles(c, rect_tiles(d[j].x0, d[j].y0, d[j].x1, d[j].y1), d[j].x0, d[j].y0, d[j].x1,
+                                       d[j].y1, d[j].times.data(), d[j].s0, n);
+            if (r) return r;
+        }
+    }
+    return RMR_OK;
+}
+
 }  // namespace
+
+// every entry point but rmr_render (and the pure getters) first launches the deferred calls, so that
+// whatever it reads, changes or orders sees them done in call order
+#define RMR_FLUSH(c)                                                   \
+    do {                                                               \
+        if (!(c)->deferred.empty()) {                                  \
+            const int rf_ = flush_calls(c);                            \
+            if (rf_) return rf_;                                       \
+        }                                                              \
+    } while (0)
 
 extern "C" {
 
@@ -945,7 +1073,8 @@ int rmr_create(rmr_ctx** out, int device) {
     rmr_default_params(&c->params);
     if (hipMalloc((void**)&c->d_queue, rmr::kQueueBytes) != hipSuccess ||
         hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_queue, 0, rmr::kQueueBytes) != hipSuccess) {   // then each fold zeroes it
         rmr_destroy(c);
         return RMR_E_HIP;
     }
@@ -973,9 +1102,11 @@ void rmr_destroy(rmr_ctx* c) {
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
     void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_esc, c->d_env, c->d_samp,
-                    c->d_tiles, c->d_times, c->d_queue, c->d_counters, c->d_srgb_thr, c->d_screen, c->d_grid, c->d_grid_list};
+                    c->d_times, c->d_queue, c->d_counters, c->d_srgb_thr, c->d_screen, c->d_grid, c->d_grid_list};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (auto& e : c->tile_cache) (void)hipFree(e.dev);
+    if (c->h_times) (void)hipHostFree(c->h_times);
     if (c->d_accum && !c->accum_external) (void)hipFree(c->d_accum);
     for (auto& k : c->jit_loaded)
         if (k.module) (void)hipModuleUnload(k.module);
@@ -987,6 +1118,7 @@ const char* rmr_last_error(const rmr_ctx* c) { return c ? c->err.c_str() : "null
 
 int rmr_set_stream(rmr_ctx* c, void* s) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     if (s) {
@@ -1001,6 +1133,7 @@ int rmr_set_stream(rmr_ctx* c, void* s) {
 
 int rmr_set_image_size(rmr_ctx* c, int w, int h) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (w <= 0 || h <= 0 || w > 32768 || h > 32768) return fail(c, RMR_E_INVALID, "bad image size");
     c->pend_W = w;
     c->pend_H = h;
@@ -1016,6 +1149,7 @@ int rmr_get_image_size(const rmr_ctx* c, int* w, int* h) {
 
 int rmr_set_params(rmr_ctx* c, const rmr_params* p) {
     if (!c || !p) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (p->max_steps < 0 || p->max_bounces < 0 || !(p->max_dist > 0.0f)) return fail(c, RMR_E_INVALID, "bad params");
     c->params = *p;
     return RMR_OK;
@@ -1030,6 +1164,7 @@ int rmr_get_params(const rmr_ctx* c, rmr_params* p) {
 int rmr_set_view(rmr_ctx* c, const float eye[3], const float r00[3], const float r01[3], const float r10[3],
                  const float r11[3]) {
     if (!c || !eye || !r00 || !r01 || !r10 || !r11) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     for (int i = 0; i < 3; i++) {
         c->view[i] = eye[i]; c->view[3 + i] = r00[i]; c->view[6 + i] = r01[i];
         c->view[9 + i] = r10[i]; c->view[12 + i] = r11[i];
@@ -1040,6 +1175,7 @@ int rmr_set_view(rmr_ctx* c, const float eye[3], const float r00[3], const float
 
 int rmr_load_scene_json(rmr_ctx* c, int variant, const char* json, size_t len) {
     if (!c || !json) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     try {
         CompiledScene s = rmr::compile_scene(std::string(json, len), variant);
         int r = validate_scene(c, s);
@@ -1056,6 +1192,7 @@ int rmr_load_scene_json(rmr_ctx* c, int variant, const char* json, size_t len) {
 
 int rmr_load_scene_tables(rmr_ctx* c, const rmr_scene* s) {
     if (!c || !s) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (s->variant < RMR_VARIANT_RM1 || s->variant > RMR_VARIANT_RM3) return fail(c, RMR_E_INVALID, "bad variant");
     if (s->n_prims < 0 || s->n_prims > RMR_MAX_PRIMS || s->n_ops < 0 || s->n_ops > RMR_MAX_OPS ||
         s->n_consts < 0 || s->n_consts > RMR_MAX_CONSTS || s->n_materials < 0 || s->n_materials > RMR_MAX_MATERIALS)
@@ -1071,6 +1208,7 @@ int rmr_load_scene_tables(rmr_ctx* c, const rmr_scene* s) {
 
 int rmr_load_builtin_scene(rmr_ctx* c, int variant) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (variant == RMR_VARIANT_RM2) return fail(c, RMR_E_SCENE, "RayMarch2.glsl needs a v2 scene for mat_func_1; use rmr_load_scene_json");
     try {
         c->scene = rmr::builtin_scene(variant);
@@ -1083,6 +1221,7 @@ int rmr_load_builtin_scene(rmr_ctx* c, int variant) {
 
 int rmr_reload(rmr_ctx* c) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->accum_external && (c->pend_W != c->W || c->pend_H != c->H))
         return fail(c, RMR_E_STATE, "bound accumulator cannot be resized");
@@ -1105,11 +1244,41 @@ int rmr_render(rmr_ctx* c, float time, float min_x, float min_y, float max_x, fl
     const int x0 = clampi((int)std::ceil(min_x), 0, c->W), y0 = clampi((int)std::ceil(min_y), 0, c->H);
     const int x1 = clampi((int)std::ceil(max_x), 0, c->W), y1 = clampi((int)std::ceil(max_y), 0, c->H);
     if (x1 <= x0 || y1 <= y0) return RMR_OK;
-    return render_tiles(c, rect_tiles(x0, y0, x1, y1), x0, y0, x1, y1, &time, current_sample, 1);
+    if (!batching_on(c)) {
+        RMR_FLUSH(c);
+        return render_tiles(c, rect_tiles(x0, y0, x1, y1), x0, y0, x1, y1, &time, current_sample, 1);
+    }
+    // deferred (rmr_set_call_batching): the errors the launch would give now come at the call
+    if (!c->scene_loaded) return fail(c, RMR_E_STATE, "no scene loaded (call rmr_load_scene_json / rmr_load_builtin_scene)");
+    if (c->params.use_env_tex && !c->d_env) return fail(c, RMR_E_STATE, "useEnvTex != 0 but no env map (rmr_set_env_map)");
+    rmr_ctx::Deferred* same = nullptr;
+    bool overlap = false;
+    for (auto& e : c->deferred) {
+        if (e.x0 == x0 && e.y0 == y0 && e.x1 == x1 && e.y1 == y1) same = &e;
+        else if (x0 < e.x1 && e.x0 < x1 && y0 < e.y1 && e.y0 < y1) overlap = true;
+    }
+    if (overlap || (same && current_sample != same->s0 + (uint32_t)same->times.size()) ||
+        (!same && c->deferred.size() >= kDeferredRectsMax)) {
+        RMR_FLUSH(c);
+        same = nullptr;
+    }
+    if (same) same->times.push_back(time);
+    else c->deferred.push_back(rmr_ctx::Deferred{x0, y0, x1, y1, current_sample, std::vector<float>(1, time)});
+    c->deferred_units += (uint64_t)((x1 - x0 + 7) / 8) * ((y1 - y0 + 7) / 8) * 64;
+    if (c->deferred_units >= kDeferredUnitsMax) RMR_FLUSH(c);
+    return RMR_OK;
+}
+
+int rmr_set_call_batching(rmr_ctx* c, int mode) {
+    if (!c || mode < -1 || mode > 1) return RMR_E_INVALID;
+    RMR_FLUSH(c);
+    c->call_batching = mode;
+    return RMR_OK;
 }
 
 int rmr_render_spp(rmr_ctx* c, const float* times, int x0, int y0, int x1, int y1, uint32_t first_sample, uint32_t nspp) {
     if (!c || (!times && nspp)) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     x0 = clampi(x0, 0, c->W); x1 = clampi(x1, 0, c->W);
     y0 = clampi(y0, 0, c->H); y1 = clampi(y1, 0, c->H);
     if (x1 <= x0 || y1 <= y0) return RMR_OK;
@@ -1120,6 +1289,7 @@ int rmr_render_tiles(rmr_ctx* c, const float* times, const int32_t* tiles_xy, in
                      uint32_t first_sample, uint32_t nspp) {
     if (!c || (!times && nspp) || (!tiles_xy && n_tiles) || tile_size <= 0 || (tile_size % 8) != 0)
         return fail(c, RMR_E_INVALID, "tile_size must be a positive multiple of 8");
+    RMR_FLUSH(c);
     // every (tx, ty) at most once: k_fold gives each pixel of a launch one thread, and a repeated
     // tile would have two threads read-modify-write the same accumulator pixel
     std::vector<std::pair<int, int>> seen;
@@ -1144,6 +1314,7 @@ int rmr_render_tiles(rmr_ctx* c, const float* times, const int32_t* tiles_xy, in
 
 int rmr_read_accum(rmr_ctx* c, float* rgba, size_t bytes) {
     if (!c || !rgba) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     const size_t need = (size_t)c->W * c->H * sizeof(float4);
     if (bytes < need) return fail(c, RMR_E_INVALID, "buffer too small");
     HIPCHK(c, hipMemcpyAsync(rgba, c->d_accum, need, hipMemcpyDeviceToHost, c->stream));
@@ -1153,6 +1324,7 @@ int rmr_read_accum(rmr_ctx* c, float* rgba, size_t bytes) {
 
 int rmr_write_accum(rmr_ctx* c, const float* rgba, size_t bytes) {
     if (!c || !rgba) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     const size_t need = (size_t)c->W * c->H * sizeof(float4);
     if (bytes < need) return fail(c, RMR_E_INVALID, "buffer too small");
     HIPCHK(c, hipMemcpyAsync(c->d_accum, rgba, need, hipMemcpyHostToDevice, c->stream));
@@ -1160,10 +1332,15 @@ int rmr_write_accum(rmr_ctx* c, const float* rgba, size_t bytes) {
     return RMR_OK;
 }
 
-void* rmr_accum_device_ptr(rmr_ctx* c) { return c ? (void*)c->d_accum : nullptr; }
+void* rmr_accum_device_ptr(rmr_ctx* c) {
+    if (!c) return nullptr;
+    if (!c->deferred.empty() && flush_calls(c) != RMR_OK) return nullptr;   // the pointer's contents include them
+    return (void*)c->d_accum;
+}
 
 int rmr_bind_accum(rmr_ctx* c, void* ptr, size_t bytes) {
     if (!c || !ptr) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (bytes < (size_t)c->W * c->H * sizeof(float4)) return fail(c, RMR_E_INVALID, "bound accumulator too small");
     if (c->d_accum && !c->accum_external) {  // the context's own buffer: free it once idle
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1177,6 +1354,7 @@ int rmr_bind_accum(rmr_ctx* c, void* ptr, size_t bytes) {
 
 int rmr_save_bmp(rmr_ctx* c, const char* path) {
     if (!c || !path) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     std::vector<float> host((size_t)c->W * c->H * 4);
     int r = rmr_read_accum(c, host.data(), host.size() * sizeof(float));
     if (r) return r;
@@ -1187,6 +1365,7 @@ int rmr_save_bmp(rmr_ctx* c, const char* path) {
 
 int rmr_save_accum(rmr_ctx* c, const char* path, uint32_t samples_done) {
     if (!c || !path) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     std::vector<float> host((size_t)c->W * c->H * 4);
     int r = rmr_read_accum(c, host.data(), host.size() * sizeof(float));
     if (r) return r;
@@ -1202,6 +1381,7 @@ int rmr_save_accum(rmr_ctx* c, const char* path, uint32_t samples_done) {
 
 int rmr_load_accum(rmr_ctx* c, const char* path, uint32_t* samples_done) {
     if (!c || !path) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     FILE* f = std::fopen(path, "rb");
     if (!f) return fail(c, RMR_E_IO, std::string("cannot open ") + path);
     char magic[8];
@@ -1224,12 +1404,14 @@ int rmr_load_accum(rmr_ctx* c, const char* path, uint32_t* samples_done) {
 
 int rmr_sync(rmr_ctx* c) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return collect_timing(c);
 }
 
 int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
     if (!c || !out) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     int r = rmr_sync(c);
     if (r) return r;
     unsigned long long cnt[16];
@@ -1243,6 +1425,7 @@ int rmr_get_stats(rmr_ctx* c, rmr_stats* out) {
 
 int rmr_get_section_cycles(rmr_ctx* c, uint64_t out[4]) {
     if (!c || !out) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     int r = rmr_sync(c);
     if (r) return r;
     unsigned long long cnt[8];
@@ -1253,6 +1436,7 @@ int rmr_get_section_cycles(rmr_ctx* c, uint64_t out[4]) {
 
 int rmr_get_counters(rmr_ctx* c, uint64_t out[16]) {
     if (!c || !out) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     int r = rmr_sync(c);
     if (r) return r;
     unsigned long long cnt[16];
@@ -1263,6 +1447,7 @@ int rmr_get_counters(rmr_ctx* c, uint64_t out[16]) {
 
 int rmr_reset_stats(rmr_ctx* c) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     int r = rmr_sync(c);
     if (r) return r;
     const double fpm = c->stats.flops_per_map;
@@ -1274,6 +1459,7 @@ int rmr_reset_stats(rmr_ctx* c) {
 
 int rmr_set_kernel(rmr_ctx* c, int kernel) {
     if (!c || kernel < 0 || kernel > 1) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     c->kernel_mode = kernel;
     return RMR_OK;
 }
@@ -1349,6 +1535,7 @@ int rmr_display(rmr_ctx* c, float centre_x, float centre_y, float zoom, float mi
         return fail(c, RMR_E_INVALID, "rmr_display: bad screen image");
     if (nbytes < (size_t)screen_w * screen_h * 4)
         return fail(c, RMR_E_INVALID, "rmr_display: screen buffer smaller than screen_w * screen_h * 4 bytes");
+    RMR_FLUSH(c);
     HIPCHK(c, hipSetDevice(c->device));
     const size_t n = (size_t)screen_w * screen_h;
     if (n > c->screen_cap) {
@@ -1373,6 +1560,7 @@ int rmr_display_device(rmr_ctx* c, float centre_x, float centre_y, float zoom, f
         return fail(c, RMR_E_INVALID, "rmr_display_device: bad screen image");
     if (nbytes < (size_t)screen_w * screen_h * 4)
         return fail(c, RMR_E_INVALID, "rmr_display_device: screen buffer smaller than screen_w * screen_h * 4 bytes");
+    RMR_FLUSH(c);
     HIPCHK(c, hipSetDevice(c->device));
     return display_common(c, centre_x, centre_y, zoom, min_x, min_y, max_x, max_y, screen_w, screen_h,
                           (uint32_t*)rgba8_dev);
@@ -1380,6 +1568,7 @@ int rmr_display_device(rmr_ctx* c, float centre_x, float centre_y, float zoom, f
 
 int rmr_set_env_map(rmr_ctx* c, const uint8_t* rgba8, int w, int h) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (!rgba8) {
         if (c->d_env) (void)hipFree(c->d_env);
         c->d_env = nullptr;
@@ -1400,6 +1589,7 @@ int rmr_set_env_map(rmr_ctx* c, const uint8_t* rgba8, int w, int h) {
 
 int rmr_set_jit(rmr_ctx* c, int mode) {
     if (!c || mode < 0 || mode > 2) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     c->jit_mode = mode;
     c->jit_failed = false;
     return RMR_OK;
@@ -1407,6 +1597,7 @@ int rmr_set_jit(rmr_ctx* c, int mode) {
 
 int rmr_set_culling(rmr_ctx* c, int flags) {
     if (!c || (flags & ~(RMR_CULL_ESCAPE | RMR_CULL_NPC | RMR_CULL_APPROX | RMR_CULL_EYE))) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (flags != c->cull) c->jit_ready = false;   // the specialised kernel depends on it
     c->cull = flags;
     return RMR_OK;
@@ -1448,6 +1639,7 @@ int rmr_jit_compile_scene(int variant, const char* json, size_t len, char* log, 
 
 int rmr_set_instrument(rmr_ctx* c, int flags) {
     if (!c || (flags & ~RMR_INSTR_COUNT_FLOPS)) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (flags != c->instrument) {
         c->instrument = flags;
         c->jit_ready = false;   // another code object (its own cache key)
@@ -1458,6 +1650,7 @@ int rmr_set_instrument(rmr_ctx* c, int flags) {
 
 int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long samp_budget_bytes) {
     if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (shade_threshold > 0) {
         c->shade_threshold = std::max(1, std::min(64, shade_threshold & 0xff));
         c->shade_auto = false;
@@ -1471,6 +1664,7 @@ int rmr_set_tuning(rmr_ctx* c, int shade_threshold, int grid_per_cu, long long s
 
 int rmr_set_grid_reserve(rmr_ctx* c, int blocks) {
     if (!c || blocks < 0) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     c->grid_reserve = blocks;
     return RMR_OK;
 }
@@ -1478,6 +1672,7 @@ int rmr_set_grid_reserve(rmr_ctx* c, int blocks) {
 // Per-sample radiance planes for parity tests: out[k][y-y0][x-x0][4] for the rect.
 int rmr_trace_samples(rmr_ctx* c, const float* times, int x0, int y0, int x1, int y1, uint32_t nspp, float* out) {
     if (!c || !times || !out) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     x0 = clampi(x0, 0, c->W); x1 = clampi(x1, 0, c->W);
     y0 = clampi(y0, 0, c->H); y1 = clampi(y1, 0, c->H);
     if (x1 <= x0 || y1 <= y0 || nspp == 0) return RMR_OK;
@@ -1514,6 +1709,8 @@ int rmr_trace_samples(rmr_ctx* c, const float* times, int x0, int y0, int x1, in
 // = the bound (+inf: none). boxes (optional, 6 floats per box, up to max_boxes) receives the inflated
 // escape boxes the kernel read, *n_boxes their number (0: the bound is off for this scene).
 int rmr_diag_ray_exit(rmr_ctx* c, const float* rays, int n, float* out, float* boxes, int max_boxes, int* n_boxes) {
+    if (!c) return RMR_E_INVALID;
+    RMR_FLUSH(c);
     if (!c->scene_loaded) return fail(c, RMR_E_STATE, "no scene loaded");
     if (n < 0 || (n > 0 && (!rays || !out))) return fail(c, RMR_E_INVALID, "bad rays / out");
     if (!c->view_set) default_view(c);

@@ -47,8 +47,11 @@ struct BvhNode {
 };
 
 // the trace kernel's work-queue counters (rmr_trace.h RMR_QUEUE_PARTS partitions, 128 B apart; room
-// for 64), zeroed before every launch
+// for 64): zero when a trace launch starts. Zeroed once at rmr_create, then by each launch's fold
+// (fold_main, after its trace on the same stream) for the next launch, so a launch costs no separate
+// memset dispatch (the reference's one-sample Graphics::Render calls: one dispatch fewer per call)
 constexpr size_t kQueueBytes = 8192;
+constexpr int kQueueWordStride = 32;   // 32-bit words between two partition counters
 
 struct KParams {
     // ---- scene tables (device pointers, read-only) ----
@@ -115,7 +118,8 @@ struct KParams {
     int32_t n_tiles;
     uint32_t nspp;              // samples in this launch
     uint32_t first_sample;      // running-mean index of sample 0
-    const float* times;         // [nspp] rand() seed per sample
+    const float* times;         // [nspp] rand() seed per sample (null when nspp == 1: time1)
+    float time1;                // the seed of a one-sample launch, as a kernel argument (no copy)
     uint64_t n_units;           // nspp * n_tiles * 64
     float4* samp;               // [nspp][n_tiles][64] per-sample radiance
     float4* accum;              // W*H running mean

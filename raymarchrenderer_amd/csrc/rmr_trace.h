@@ -766,6 +766,11 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 #ifndef RMR_NPC_DP_LDS
 #define RMR_NPC_DP_LDS -1
 #endif
+// the generator states the scene's primitive count with an LDS choice (rmr_jit.cpp): the LDS table of
+// trace_main (s_dp, 2 x RMR_NPC_LDS_MAX float4) must hold every one of them
+#if defined(RMR_NPC_NPRIMS) && RMR_NPC_DP_LDS == 1
+static_assert(RMR_NPC_NPRIMS <= RMR_NPC_LDS_MAX, "RMR_NPC_DP_LDS=1 with more primitives than the LDS table holds");
+#endif
 RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j) {
     const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type|index<<8 mat_id
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
@@ -1370,7 +1375,7 @@ RMR_D bool trace_prologue(const KParams& P, Lane& L, V3 dir, float te_pre = __bu
     return false;
 }
 
-// unit -> (sample k, pixel); false if the pixel is outside the clip rect
+// unit -> (sample k, pixel); false if the pixel is outside the launch's clip rect
 RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& time) {
     const uint32_t per_k = (uint32_t)P.n_tiles * 64u;
     const uint32_t k = u / per_k;
@@ -1379,7 +1384,7 @@ RMR_D bool unit_pixel(const KParams& P, uint32_t u, int& px, int& py, float& tim
     const TileXY txy = P.tiles[tile];
     px = txy.x + (lane & 7);
     py = txy.y + (lane >> 3);
-    time = P.times[k];
+    time = P.nspp == 1u ? P.time1 : P.times[k];
     return !(px < P.x0 || py < P.y0 || px >= P.x1 || py >= P.y1);
 }
 
@@ -2268,6 +2273,7 @@ constexpr int trace_waves() {
 #define RMR_QUEUE_SEQ 1   // small launches: partitions a wave tries in turn before it reads every counter
 #endif
 #define RMR_QUEUE_STRIDE 32   // 32-bit words between two partition counters (128 B)
+static_assert(RMR_QUEUE_STRIDE == kQueueWordStride, "fold_main zeroes the counters at this stride");
 static_assert(RMR_QUEUE_PARTS >= 1 && RMR_QUEUE_PARTS <= 64 && RMR_QUEUE_PARTS * RMR_QUEUE_STRIDE * 4 <= (int)kQueueBytes,
               "queue counters: one per lane of the scan");
 #ifndef RMR_CHUNK_CACHE
@@ -2777,6 +2783,9 @@ RMR_D void trace_main(const KParams& P) {
 // Running mean of main(), RM1:600-612: new = c/(n+1) + old*n/(n+1), sample order k = 0..nspp-1.
 RMR_D void fold_main(const KParams& P) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    // the trace launch before this fold (same stream) is complete: zero its work-queue counters (every
+    // one of the 64 the queue has room for) for the next launch (rmr_internal.h kQueueBytes)
+    if (gid < (int)(kQueueBytes / (4 * kQueueWordStride))) ((uint32_t*)P.queue)[gid * kQueueWordStride] = 0u;
     const int tile = gid >> 6, lane = gid & 63;
     if (tile >= P.n_tiles) return;
     const TileXY txy = P.tiles[tile];

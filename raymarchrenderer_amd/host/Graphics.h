@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/rmr.h"
+#include "../../include/rmr_group.h"
 #include "Vector.h"
 
 class Graphics {
@@ -46,6 +47,17 @@ public:
     static void setParams(const rmr_params& p);
     static rmr_params getParams();
     static void setDevice(int device);
+    // Several GPUs of the node from this process (librmr_group.so, include/rmr_group.h): call before
+    // Init. Init then creates a device group instead of one context; setView / setParams / setEnvMap /
+    // Reload go to every GPU, RenderFrame renders whole frames tile-partitioned over them with one RCCL
+    // reduce each, and SaveImage writes the last such frame. (Render / RenderSamples draw on the first
+    // GPU's context alone.) One device is a valid group: the RCCL path with a single rank.
+    static void setDevices(const std::vector<int>& devices);
+    // One whole frame of samples 0 .. nspp-1 (times[k] seeds sample k): on the device group when
+    // setDevices was given, else rmr_render_spp of the whole image on the one context. Bitwise the
+    // same image either way.
+    static void RenderFrame(const float* times, unsigned nspp);
+    static rmr_group* group();  // the device group (nullptr without setDevices)
     // envTex of skyColor (Graphics.cpp:287 loads it from data/textures/veranda_1k.hdr): RGBA8, row
     // 0 = up; used when the params' use_env_tex is set. nullptr removes it.
     static void setEnvMap(const unsigned char* rgba8, int w, int h);

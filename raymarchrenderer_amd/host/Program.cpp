@@ -11,7 +11,11 @@
 //  * by default a tile's samples go to the GPU in one batched call (Graphics::RenderSamples,
 //    bitwise equal to the per-sample calls); --per-sample issues one Graphics::Render per sample
 //    per tile exactly like the reference;
-//  * save() writes output/<%Y-%m-%d_%H-%M-%S>.bmp (Program.cpp:71-84) unless --out is given.
+//  * save() writes output/<%Y-%m-%d_%H-%M-%S>.bmp (Program.cpp:71-84) unless --out is given;
+//  * --gpus N / --devices a,b,..: the frame tile-partitioned over several GPUs of the node from this one
+//    process (Graphics::setDevices -> librmr_group.so, one RCCL reduce per frame): the whole image
+//    rendered as one frame of `samples` samples (or `passes` in progressive mode), bitwise the image
+//    the tile loop gives wherever the grid covers it (every pixel gets the same seeds in the same order).
 #include <sys/stat.h>
 #include <dirent.h>
 
@@ -49,6 +53,7 @@ struct Options {
     int grid_w = 4, grid_h = 4;     // Program.cpp:106-107
     int frame = 0;
     int device = 0;
+    std::vector<int> devices;       // --gpus / --devices: the device group
     bool per_sample = false, interactive = false, quiet = false;
     bool print_tiles = false, print_view = false;  // host-only diagnostics (no GPU needed)
     rmr_params params;
@@ -184,6 +189,17 @@ RenderResult render(const Options& o, unsigned first_pass) {
         mn = Vector2(t.first * cw, t.second * ch);
         mx = Vector2((t.first + 1) * cw, (t.second + 1) * ch);
     };
+    if (!o.devices.empty()) {   // the device group: one frame over the whole image
+        const unsigned n = o.samples > 0 ? (unsigned)o.samples : (unsigned)o.passes;
+        std::vector<float> times(n);
+        for (unsigned s = 0; s < n; s++) times[s] = seed_time(o.frame, s);
+        Graphics::RenderFrame(times.data(), n);
+        if (Graphics::lastStatus() != RMR_OK) return r;
+        Graphics::Sync();
+        r.samples = (unsigned long long)n * (unsigned long long)W * H;
+        r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return r;
+    }
     if (o.samples > 0) {
         std::vector<float> times(o.samples);
         for (int s = 0; s < o.samples; s++) times[s] = seed_time(o.frame, s);
@@ -311,7 +327,8 @@ void usage() {
         "  --per-sample        one Graphics::Render launch per sample per tile (reference pattern)\n"
         "  --out FILE.bmp      (default output/<timestamp>.bmp)\n"
         "  --checkpoint FILE   write the float accumulator at the end; --resume FILE continue from one\n"
-        "  --device N  --interactive (CLI.cpp commands on stdin)  --scene-dir DIR  --quiet");
+        "  --device N  --interactive (CLI.cpp commands on stdin)  --scene-dir DIR  --quiet\n"
+        "  --gpus N | --devices a,b,..  the frame tile-partitioned over those GPUs (one process, RCCL reduce)");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -352,6 +369,18 @@ bool parse(int argc, char** argv, Options& o) {
         else if (a == "--checkpoint") o.checkpoint = next("--checkpoint");
         else if (a == "--resume") o.resume = next("--resume");
         else if (a == "--device") o.device = std::atoi(next("--device"));
+        else if (a == "--gpus") {
+            const int n = std::atoi(next("--gpus"));
+            if (n <= 0) return false;
+            o.devices.clear();
+            for (int d = 0; d < n; d++) o.devices.push_back(d);
+        } else if (a == "--devices") {
+            std::stringstream ss(next("--devices"));
+            std::string item;
+            o.devices.clear();
+            while (std::getline(ss, item, ',')) o.devices.push_back(std::atoi(item.c_str()));
+            if (o.devices.empty()) return false;
+        }
         else if (a == "--interactive") o.interactive = true;
         else if (a == "--scene-dir") o.scene_dir = next("--scene-dir");
         else if (a == "--quiet") o.quiet = true;
@@ -398,6 +427,13 @@ int main(int argc, char** argv) {
     }
     Screen::setScreenSize(Vector2(1280, 720));  // Program.cpp:89
     Graphics::setDevice(o.device);
+    if (!o.devices.empty()) {
+        if (!o.checkpoint.empty() || !o.resume.empty() || o.interactive) {
+            std::fprintf(stderr, "--gpus / --devices: no checkpoint, resume or interactive mode\n");
+            return 2;
+        }
+        Graphics::setDevices(o.devices);
+    }
     Graphics::setVariant(o.variant);
     Graphics::setImageSize(Vector2(o.width, o.height));
     if (!o.scene.empty() && !load_scene(o.scene)) return 1;

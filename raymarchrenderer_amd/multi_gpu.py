@@ -49,6 +49,15 @@ def tile_costs(renderer, tiles, tile, times):
     return cost
 
 
+def frame_tile_costs(renderer, W, H, tile, times):
+    """tile_costs over every tile of the frame, as {(tx, ty): map evals}: one probe that every rank
+    share of a partition can slice (FrameRenderer.order_tiles_by_cost cost_map) instead of probing its
+    tiles again for each rank count. Writes the renderer's accumulator."""
+    tiles = frame_tiles(W, H, tile)
+    cost = tile_costs(renderer, tiles, tile, times)
+    return {t: int(c) for t, c in zip(tiles, cost)}
+
+
 def _multi(dist, group=None, always=False):
     return dist is not None and dist.is_initialized() and (always or dist.get_world_size(group) > 1)
 
@@ -82,10 +91,13 @@ class FrameRenderer:
     def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None,
                  reduce_at_world1=False, grid_reserve=OVERLAP_GRID_RESERVE):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
+        self._saved_reserve = []
         if render_fn is None and len(self.rs) > 1 and grid_reserve is not None:
             # overlapping contexts: each trace launch leaves a few workgroup slots free, so the other
-            # context's fold and zeroing run beside it instead of waiting for its drain (rmr.h)
+            # context's fold and zeroing run beside it instead of waiting for its drain (rmr.h); the
+            # renderers' own settings come back at close()
             for r in self.rs:
+                self._saved_reserve.append((r, r.grid_reserve))
                 r.set_grid_reserve(grid_reserve)
         self.r, self.dist, self.render_fn = self.rs[0], dist, render_fn
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
@@ -131,7 +143,7 @@ class FrameRenderer:
         self.last = acc
         return acc
 
-    def order_tiles_by_cost(self, times, min_spread=3.0, frame_times=None, trials=4):
+    def order_tiles_by_cost(self, times, min_spread=3.0, frame_times=None, trials=4, cost_map=None):
         """Hand this rank's costliest tiles out first where that makes frames faster. The work queue
         gives units out in tile-list order within each sample, so a launch ends (drains) on its last
         tiles' paths; with the cheap ones last (by each tile's map() evaluations in a probe over
@@ -142,11 +154,14 @@ class FrameRenderer:
         (tile costs up to 5x the mean) +2.7%, the RM2 NEE frame (sky tiles) -11%, Cornell-5 / C5 / RM3
         (under 2x) within noise. Each pixel's samples are the same whatever the order, so the image is
         the same bits. Call before the first frame (the probe writes the first accumulator, which every
-        frame zeroes). Returns whether it reordered."""
+        frame zeroes). `cost_map` ({(tx, ty): cost}, frame_tile_costs): costs probed once for the whole
+        frame, sliced to this rank's tiles instead of probed again. Returns whether it reordered."""
         if self.render_fn is not None:
             return False
         cost = np.zeros(0, np.int64)
-        if len(self.tiles):
+        if len(self.tiles) and cost_map is not None:
+            cost = np.array([cost_map[(int(tx), int(ty))] for tx, ty in self.tiles], np.int64)
+        elif len(self.tiles):
             acc = self.accs[0]
             with self._on_stream(0):
                 self.r.bind_accum(acc.data_ptr(), acc.numel() * acc.element_size())
@@ -216,3 +231,12 @@ class FrameRenderer:
                     w.wait()
                 self.work[i] = None
         return self.last
+
+    def close(self):
+        """finish(), then give the renderers back their grid reserve from before this FrameRenderer
+        (the passed contexts can be used on their own or in another FrameRenderer afterwards)."""
+        last = self.finish()
+        for r, v in self._saved_reserve:
+            r.set_grid_reserve(v)
+        self._saved_reserve = []
+        return last

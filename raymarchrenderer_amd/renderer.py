@@ -168,6 +168,12 @@ class Renderer:
     def set_grid_reserve(self, blocks):
         """Workgroups the persistent trace launch leaves free (rmr_set_grid_reserve; scheduling only)."""
         self._chk(self._L.rmr_set_grid_reserve(self._ctx, int(blocks)))
+        self._grid_reserve = int(blocks)
+
+    @property
+    def grid_reserve(self):
+        """The reserve last set through this object (0, the context's default, until then)."""
+        return getattr(self, "_grid_reserve", 0)
 
     def set_env_map(self, rgba8):
         """envTex for skyColor (used with params use_env_tex=1): (h, w, 4) uint8, row 0 = up. None clears."""
@@ -199,6 +205,11 @@ class Renderer:
         """Graphics::Render(currentTime, min, max, currentSample)."""
         self._chk(self._L.rmr_render(self._ctx, float(time), float(vmin[0]), float(vmin[1]),
                                            float(vmax[0]), float(vmax[1]), int(current_sample)))
+
+    def set_call_batching(self, mode):
+        """rmr_set_call_batching: 1 on, 0 off, -1 auto (the default: on while the context owns its stream
+        and accumulator). Batched render() calls go to the GPU together at the next other call."""
+        self._chk(self._L.rmr_set_call_batching(self._ctx, int(mode)))
 
     def render_spp(self, times, rect=None, first_sample=0):
         times = np.ascontiguousarray(times, np.float32)

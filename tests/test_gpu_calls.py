@@ -1,0 +1,131 @@
+"""The reference's call pattern through the drop-in: one Graphics::Render (rmr_render) call per tile and
+sample (Program.cpp:184-284), with the library's call batching (rmr_set_call_batching) on and off.
+
+Batched calls must give the bits of the same calls made one launch each, and of the oracle: every
+pixel's samples, seeds and running-mean order are the same whatever launch carries them. The tile
+grids here do not divide into 8x8 tiles (per-tile clipping, rmr_api.cpp tile_at), and the calls
+interleave with the entry points that flush them."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from raymarchrenderer_amd import Renderer, abi, tile_spiral, time_schedule
+
+from .conftest import SCENES
+from .test_gpu_parity import _setup, _tables, same_bits
+
+pytestmark = pytest.mark.gpu
+
+CORNELL = os.path.join(SCENES, "cornell5.scene")
+
+
+def _rects(W, H, gw, gh):
+    cw, ch = W // gw, H // gh   # Program.cpp:108-109
+    return [((x * cw, y * ch), ((x + 1) * cw, (y + 1) * ch)) for x, y in tile_spiral(gw, gh)]
+
+
+def _fixed(r, rects, times):
+    """Program.cpp:232-284: every tile's samples before the next tile."""
+    for mn, mx in rects:
+        for s, t in enumerate(times):
+            r.render(float(t), mn, mx, s)
+
+
+def _progressive(r, rects, times):
+    """Program.cpp:184-231: one sample of every tile per pass."""
+    for s, t in enumerate(times):
+        for mn, mx in rects:
+            r.render(float(t), mn, mx, s)
+
+
+@pytest.mark.parametrize("pattern", ["fixed", "progressive"])
+def test_call_batching_bitwise(renderer, pattern):
+    W, H, gw, gh = 62, 45, 3, 4          # 20 x 11 pixel tiles: no tile edge on the 8x8 grid
+    prm, view = _setup(renderer, CORNELL, "rm1", W, H, {"max_bounces": 3})
+    times = time_schedule(3, frame=2)
+    rects = _rects(W, H, gw, gh)
+    run = _fixed if pattern == "fixed" else _progressive
+    out, launches = {}, {}
+    try:
+        for mode in (0, 1):
+            renderer.set_call_batching(mode)
+            renderer.reload()
+            renderer.reset_stats()
+            run(renderer, rects, times)
+            out[mode] = renderer.read_accum()
+            launches[mode] = renderer.stats().trace_launches
+    finally:
+        renderer.set_call_batching(-1)
+    assert launches[0] == len(rects) * len(times)
+    assert launches[1] == 1   # every rect holds the same samples: one launch over their union
+    assert same_bits(out[0], out[1]).all()
+    cw, ch = W // gw, H // gh
+    cpu = oracle.Oracle(_tables(CORNELL, "rm1"), prm, view, W, H).render(times, rect=(0, 0, cw * gw, ch * gh))
+    assert same_bits(out[1], cpu).all()
+    assert (out[1][ch * gh:] == 0).all() and (out[1][:, cw * gw:] == 0).all()   # the grid's remainder
+
+
+def test_call_batching_order_and_flush_points(renderer):
+    """Overlapping rects, a sample out of sequence and reads between calls: the batched context gives
+    the bits of the one-launch-per-call context at every read."""
+    W, H = 40, 32
+    _setup(renderer, CORNELL, "rm1", W, H, {"max_bounces": 2})
+    times = time_schedule(6, frame=3)
+    calls = [  # (time index, min, max, current_sample)
+        (0, (0, 0), (24, 20), 0), (1, (0, 0), (24, 20), 1),
+        (2, (16, 8), (40, 32), 0),            # overlaps the first rect: flush, then hold
+        (3, (16, 8), (40, 32), 1), (4, (0, 0), (24, 20), 2),   # back to the first rect
+        "read",
+        (5, (0, 0), (24, 20), 3), (0, (0, 24), (12, 32), 0),   # a disjoint rect joins
+        (1, (0, 24), (12, 32), 5),            # sample index out of sequence: flush first
+        "read",
+        (2, (3.5, 1.2), (9.7, 30.0), 0),      # fractional bounds (RM1:572 pix >= min && pix < max)
+    ]
+    seen = {}
+    try:
+        for mode in (0, 1):
+            renderer.set_call_batching(mode)
+            renderer.reload()
+            reads = []
+            for c in calls:
+                if c == "read":
+                    reads.append(renderer.read_accum())
+                else:
+                    k, mn, mx, s = c
+                    renderer.render(float(times[k]), mn, mx, s)
+            reads.append(renderer.read_accum())
+            seen[mode] = reads
+    finally:
+        renderer.set_call_batching(-1)
+    for a, b in zip(seen[0], seen[1]):
+        assert same_bits(a, b).all()
+
+
+def test_call_batching_is_off_on_a_caller_stream_and_reports_errors_at_the_call():
+    """Auto mode batches only while the context owns its stream; a state error (no scene) is returned by
+    the call itself, not by a later flush."""
+    import torch
+    r = Renderer(0, 16, 16)
+    try:
+        with pytest.raises(Exception) as e:
+            r.render(0.0, (0, 0), (16, 16), 0)
+        assert "no scene" in str(e.value)
+        r.load_scene(CORNELL, "rm1")
+        r.set_params(abi.default_params(max_bounces=1))
+        r.reset_stats()
+        r.render(0.0, (0, 0), (16, 16), 0)
+        assert r.stats().trace_launches == 1   # flushed by rmr_get_stats
+        # a caller's stream and accumulator (FrameRenderer's way): the call's launch is on that stream
+        # when rmr_render returns, so the caller's own work ordered after it sees the sample
+        s = torch.cuda.Stream()
+        acc = torch.zeros((16, 16, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.set_stream(s.cuda_stream)
+        r.bind_accum(acc.data_ptr(), acc.numel() * 4)
+        r.render(0.1, (0, 0), (16, 16), 0)
+        s.synchronize()   # no rmr call in between
+        assert (acc[..., 3] == 1.0).all().item()
+    finally:
+        r.close()

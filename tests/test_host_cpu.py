@@ -154,3 +154,37 @@ def test_embedded_kernel_sources_drop_comments_only():
     assert got.count("\n") == mac.count("\n")
     assert got.splitlines()[0].endswith("\\") and "+ 1" in got.splitlines()[1]
     assert strip("int a; /* x\ny */ int b;\n") == "int a;\n int b;\n"
+
+
+def test_group_library_exports_every_header_symbol():
+    """librmr_group.so (include/rmr_group.h): the multi-GPU device group of the C++ host."""
+    from raymarchrenderer_amd.group import GROUP_EXPORTS, group_lib
+    hdr = open(os.path.join(ROOT, "include", "rmr_group.h")).read()
+    declared = set(re.findall(r"\b(rmr_group_[a-z_0-9]+)\s*\(", hdr))
+    L = group_lib()
+    for name in sorted(declared):
+        assert hasattr(L, name), name
+    assert declared == set(GROUP_EXPORTS)
+
+
+@pytest.mark.parametrize("W,H,tile,n", [(1920, 1080, 32, 8), (1920, 1080, 32, 3), (3840, 2160, 64, 8),
+                                         (64, 48, 16, 2), (100, 70, 32, 5), (8, 8, 32, 4)])
+def test_group_partition_equals_tile_partition(W, H, tile, n):
+    """The C++ group's partition (rmr_group_partition) is multi_gpu.tile_partition, member by member:
+    the single-process group and the one-process-per-GPU path split a frame the same way."""
+    from raymarchrenderer_amd.group import group_partition
+    from raymarchrenderer_amd.multi_gpu import frame_tiles, tile_partition
+    seen = []
+    for m in range(n):
+        got = group_partition(W, H, tile, m, n)
+        want = tile_partition(W, H, tile, m, n)
+        assert got.shape == want.shape and (got == want).all()
+        seen += [tuple(t) for t in got]
+    assert sorted(seen) == sorted(frame_tiles(W, H, tile))   # every tile once
+
+
+def test_group_partition_rejects_bad_arguments():
+    from raymarchrenderer_amd.group import group_lib
+    L = group_lib()
+    for args in [(0, 10, 32, 0, 1), (10, 10, 0, 0, 1), (10, 10, 32, 1, 1), (10, 10, 32, -1, 2), (10, 10, 32, 0, 0)]:
+        assert L.rmr_group_partition(*args, None, 0) < 0
