@@ -771,8 +771,21 @@ RMR_D float npc_eps(const KParams& P, V3 p) {
 #if defined(RMR_NPC_NPRIMS) && RMR_NPC_DP_LDS == 1
 static_assert(RMR_NPC_NPRIMS <= RMR_NPC_LDS_MAX, "RMR_NPC_DP_LDS=1 with more primitives than the LDS table holds");
 #endif
-RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j) {
-    const float4 a = q[0], b = q[1];  // c.xyz r.x | r.yz type|index<<8 mat_id
+// Layout of the table the cache kernel gathers from per lane (dtab / s_dp): entry k is two float4 (a, b).
+// AoS (a at [2k], b at [2k + 1]): the global P.dprims and the ahead-of-time kernels' LDS copy. SoA for the
+// hipRTC cache kernels' LDS copy (RMR_NPC_TAB_SOA, rmr_jit.cpp): a at [k], b at [k + RMR_NPC_LDS_MAX].
+// A ds_read_b128 serves 16 lanes per LDS cycle from one 256-B bank row of 16 16-B slots; with 32-B
+// entries every a (and every b) sits in an even (odd) slot, so 16 lanes gathering random entries
+// share 8 slots, against 16 with 16-B entries (C4's profile: 1.7 bank-conflict cycles per LDS
+// instruction, r05_attr_c4_ds.json)
+#ifndef RMR_NPC_TAB_SOA
+#define RMR_NPC_TAB_SOA 0
+#endif
+static_assert(!RMR_NPC_TAB_SOA || RMR_NPC_DP_LDS == 1, "the SoA table is the compile-time LDS copy");
+constexpr int kTabStep = RMR_NPC_TAB_SOA ? 1 : 2;               // float4s from entry k to entry k + 1
+constexpr int kTabHi = RMR_NPC_TAB_SOA ? RMR_NPC_LDS_MAX : 1;   // float4s from an entry's a to its b
+RMR_D float prim_dist_at(const float4* q, V3 p, float& mid, int& j, int hi = 1) {
+    const float4 a = q[0], b = q[hi];  // c.xyz r.x | r.yz type|index<<8 mat_id (hi: kTabHi for a table)
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
     const V3 c = v3(a.x, a.y, a.z);
     const V3 h = box ? v3(a.w, b.x, b.y) : v3s(0.0f);
@@ -804,7 +817,7 @@ RMR_D void npc_pack_entry(float4& a, float4& b) {
     b = nb;
 }
 RMR_D float prim_dist_packed(const float4* q, V3 p, float& mid, int& j) {
-    const float4 a = q[0], b = q[1];
+    const float4 a = q[0], b = q[kTabHi];
     mid = am_id_of(b.w);
     j = am_w_of(b.w);
     const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - v3(b.x, b.y, b.z);
@@ -814,7 +827,7 @@ RMR_D float prim_dist_packed(const float4* q, V3 p, float& mid, int& j) {
 // prim_dist_at on the table the cache kernel reads (dtab / the LDS copy)
 RMR_D float prim_dist_tab(const float4* q, V3 p, float& mid, int& j) {
     if constexpr (kNpcPacked) return prim_dist_packed(q, p, mid, j);
-    else return prim_dist_at(q, p, mid, j);
+    else return prim_dist_at(q, p, mid, j, kTabHi);
 }
 // Primitives per lane in the nearest-primitive cache (1 or 2): with 2 the cache holds the two
 // nearest primitives and bounds every other one (a ray passing between two neighbours keeps them).
@@ -1049,7 +1062,7 @@ RMR_D void npc_insert(float a, int k, float& u1, float& u2, float& u3, int& k1, 
 // approximate distance of leaf-order primitive k (per-lane index; am_prim's value: a sphere is the
 // box of half-extent 0 minus its radius, as prim_dist_at)
 RMR_D float am_prim_at(const float4* q, V3 p) {
-    const float4 a = q[0], b = q[1];   // c.xyz r.x | r.yz type|index<<8 mat_id
+    const float4 a = q[0], b = q[kTabHi];   // c.xyz r.x | r.yz type|index<<8 mat_id (table entry)
     const bool box = (__float_as_int(b.z) & 0xff) == RMR_PRIM_BOX;
     const V3 h = box ? v3(a.w, b.x, b.y) : v3s(0.0f);
     const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - h;
@@ -1070,7 +1083,7 @@ RMR_D float am_sphere_at(const float4* q, V3 p) {
 #endif
 // am_prim_at on the packed LDS table (kNpcPacked)
 RMR_D float am_prim_packed(const float4* q, V3 p) {
-    const float4 a = q[0], b = q[1];
+    const float4 a = q[0], b = q[kTabHi];
     const V3 qq = vabs(p - v3(a.x, a.y, a.z)) - v3(b.x, b.y, b.z);
     const float k0 = fminf(fmaxf(qq.x, fmaxf(qq.y, qq.z)), 0.0f);
     const V3 o = vmax0(qq);
@@ -1160,12 +1173,12 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
             const int k = (int)(((i < 2 ? cell.z : cell.w) >> (16 * (i & 1))) & 0xffffu);
-            if (i < n && k != ks) npc_insert(RMR_AM_LISTED(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
+            if (i < n && k != ks) npc_insert(RMR_AM_LISTED(dtab + kTabStep * k, p), k, u1, u2, u3, k1, k2);
         }
         for (uint32_t i = 4; i < n; i++) {
             const int k = (int)P.grid_list[off + i];
             if (k == ks) continue;
-            npc_insert(RMR_AM_LISTED(dtab + 2 * k, p), k, u1, u2, u3, k1, k2);
+            npc_insert(RMR_AM_LISTED(dtab + kTabStep * k, p), k, u1, u2, u3, k1, k2);
         }
         RMR_COUNT(P.counters, active_lanes(), 12, 1);   // (the count build prices a listed primitive as a sphere)
         const float margin = fmaf(fabsf(u1) + fabsf(u2) + R2, 0x1p-20f, 0x1p-39f);
@@ -1174,7 +1187,7 @@ RMR_D V2 map_grid_npc(const KParams& P, V3 p, int& kw, int& kw2, float& sb, int 
         if (uniq) {
             float mid;
             int j;
-            const float dw = (k1 == ks) ? ds : prim_dist_tab(dtab + 2 * k1, p, mid, j);
+            const float dw = (k1 == ks) ? ds : prim_dist_tab(dtab + kTabStep * k1, p, mid, j);
             if (k1 == ks) mid = ms;
             opu(d, dw, mid);
             kw = (dw > P.max_dist) ? -1 : k1;
@@ -1737,7 +1750,7 @@ RMR_D void cert_normals(const KParams& P, Lane& L, bool mine, uint64_t cm, int* 
         const V3 e = v3(sg * (ax == 0 ? 0.001f : 0.0f), sg * (ax == 1 ? 0.001f : 0.0f), sg * (ax == 2 ? 0.001f : 0.0f));
         float mid;
         int j;
-        const float F = prim_dist_tab(dtab + 2 * (act ? w : 0), v3(hx, hy, hz) + e, mid, j);
+        const float F = prim_dist_tab(dtab + kTabStep * (act ? w : 0), v3(hx, hy, hz) + e, mid, j);
         const float val = (P.max_dist >= F) ? F : P.max_dist;   // opu(d = (maxDist, -1), F, .).x
 #pragma unroll
         for (int k = 0; k < 6; k++) {   // owners collect the values of this pass
@@ -2191,6 +2204,39 @@ RMR_D uint32_t lane_now() {
     return v;
 }
 
+// The nearest-primitive cache's state after a full map() at p: primitives kw, kw2 (kw < 0: none) and the
+// lower bound s2 of every other primitive's distance (MAP::full); |s2| 2^-20: the rounding of the
+// check's own subtractions
+RMR_D void npc_apply(const KParams& P, Lane& L, V3 p, int kw, int kw2, float s2) {
+    L.cw = kw >= 0 ? kw : 0;
+    L.cw2 = kw >= 0 ? kw2 : 0;
+    L.cs = kw >= 0 ? s2 - fmaf(fabsf(s2), 0x1p-20f, npc_eps(P, p)) - (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
+                   : -__builtin_inff();
+    L.cta = L.t;
+}
+
+// the position of the (r + 1)-th lowest set bit of m (r < popcount(m)), per lane: a binary search on
+// the counts of the lower halves (the block pool's request assignment)
+RMR_D int nth_set_bit(uint64_t m, uint32_t r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = m & ((1ull << w) - 1ull);
+        const uint32_t c = (uint32_t)__popcll(low);
+        const bool up = r >= c;
+        r = up ? r - c : r;
+        m = up ? (m >> w) : low;
+        pos += up ? w : 0;
+    }
+    return pos;
+}
+
+// a 64-bit value made wave-uniform (SGPRs); readfirstlane returns int: through uint32_t, not sign-extended
+RMR_D uint64_t rfl64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 // a defined value the compiler cannot see (no constant to propagate into the loop PHIs): trace_main's
 // lane at kernel entry; the inline asm emits no instruction
 RMR_D float opq() {
@@ -2279,6 +2325,28 @@ static_assert(RMR_QUEUE_PARTS >= 1 && RMR_QUEUE_PARTS <= 64 && RMR_QUEUE_PARTS *
 #ifndef RMR_CHUNK_CACHE
 #define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
+// Block-level pool of the nearest-primitive cache's full map() requests (the hipRTC cache kernels whose
+// primitive table is the compile-time LDS copy, RMR_NPC_TAB_SOA). Without it a wave runs the full map
+// (candidate grid cell + list, or the BVH) for its own lanes whose cache bound failed, once enough of
+// them wait: 28 lanes per batch on average (r06 C4 profile), in batches that take 38% of the waves'
+// cycles. With it a lane whose bound fails posts its point and cached primitive (16 B) to the block's
+// pool in LDS and waits; a wave that serves takes up to 64 requests of any of the block's four waves,
+// runs their full maps 64 wide and posts the results (16 B each) back; the owner lanes pick them up at
+// their next iteration. Only the point and the result move, no path state. The same full map() on the
+// same inputs, so the same bits. The pool's 4 KiB come from 32-unit work chunks (RMR_CHUNK_POOL), so
+// the kernel stays at 6 blocks per CU.
+#ifndef RMR_NPC_POOL
+#define RMR_NPC_POOL 1
+#endif
+#ifndef RMR_CHUNK_POOL
+#define RMR_CHUNK_POOL 32
+#endif
+#ifndef RMR_POOL_SLEEP
+#define RMR_POOL_SLEEP 1
+#endif
+#ifndef RMR_POOL_SERVE
+#define RMR_POOL_SERVE 56   // pending requests in the block at which a wave serves (up to 64 of them)
+#endif
 typedef uint32_t WCount;
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
@@ -2302,7 +2370,9 @@ RMR_D void trace_main(const KParams& P) {
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
     WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, bmaps = 0;
-    constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
+    constexpr bool kPool = MAP::kCache && HO && RMR_NPC_POOL && RMR_NPC_TAB_SOA;   // RMR_NPC_POOL above
+    constexpr uint32_t CHUNK = MAP::kCache ? (kPool ? RMR_CHUNK_POOL : RMR_CHUNK_CACHE) : RMR_CHUNK;
+    bool waiting = false;   // kPool: this lane's full map() request is in the block's pool
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
     // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
@@ -2346,6 +2416,7 @@ RMR_D void trace_main(const KParams& P) {
     }
 #ifdef RMR_PROFILE
     uint64_t cyc[4] = {0, 0, 0, 0};   // refill, map() iterations, shading, cache kernels: full map() batches
+    uint64_t full_lanes = 0;           // cache kernels: lanes in the full map() batches
     const uint64_t c_begin = __builtin_amdgcn_s_memtime();
 #define RMR_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #else
@@ -2358,6 +2429,16 @@ RMR_D void trace_main(const KParams& P) {
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
+    // kPool: one request / result slot per lane of the block (p.xyz, seed leaf index | m.x, m.y, s2,
+    // kw | kw2 << 16) and, per wave, the bits of its lanes whose request is pending / result is ready
+    __shared__ float4 s_pool[kPool ? 256 : 1];
+    __shared__ unsigned long long s_pend[kPool ? 4 : 1], s_rdy[kPool ? 4 : 1];
+    if constexpr (kPool) {
+        if (threadIdx.x < 4) {
+            s_pend[threadIdx.x] = 0ull;
+            s_rdy[threadIdx.x] = 0ull;
+        }
+    }
     // the stepped Mandelbulb kernel (8 waves / SIMD, 20 KiB of LDS per block): the RNG state (seeds
     // gx + time, gy + time and the chain value randChange), which only shading reads and advances,
     // waits in LDS between shading batches instead of in registers the allocator spilled to scratch
@@ -2372,15 +2453,17 @@ RMR_D void trace_main(const KParams& P) {
             for (int i = (int)threadIdx.x; i < P.n_prims; i += (int)blockDim.x) {
                 float4 a = ((const float4*)P.dprims)[2 * i], b = ((const float4*)P.dprims)[2 * i + 1];
                 npc_pack_entry(a, b);
-                s_dp[2 * i] = a;
-                s_dp[2 * i + 1] = b;
+                s_dp[kTabStep * i] = a;
+                s_dp[kTabStep * i + kTabHi] = b;
             }
         } else {
-            for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x) s_dp[i] = ((const float4*)P.dprims)[i];
+            for (int i = (int)threadIdx.x; i < 2 * P.n_prims; i += (int)blockDim.x)
+                s_dp[kTabStep * (i >> 1) + (i & 1) * kTabHi] = ((const float4*)P.dprims)[i];
         }
         __syncthreads();
     }
-#define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_tab(s_dp + 2 * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
+#define RMR_PRIM_DIST(k, p, mid, j) (dp_lds ? prim_dist_tab(s_dp + kTabStep * (k), p, mid, j) : prim_dist(P, k, p, mid, j))
+    static_assert(!RMR_NPC_TAB_SOA || MAP::kCache, "an SoA table kernel reads dtab as the LDS copy only");
 #define RMR_DTAB (dp_lds ? (const float4*)s_dp : (const float4*)P.dprims)
     const int wv = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);   // the wave's index in its block (an SGPR)
     uint32_t chunk_base = 0;
@@ -2522,7 +2605,27 @@ RMR_D void trace_main(const KParams& P) {
                 float F = 0.0f, mid = -1.0f;
                 int jw = 0;
                 bool pfin = false;   // a point without NaN (and without +-inf of both signs)
-                if (act1) {
+                bool got = false;    // kPool: this lane's full map() result came back from the block's pool
+                if constexpr (kPool) {
+                    if (__ballot(waiting)) {
+                        const uint64_t rdy = rfl64(__hip_atomic_load(s_rdy + wv, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        got = waiting && ((rdy >> lane_now()) & 1ull) != 0;
+                        const uint64_t gm = __ballot(got);
+                        if (gm) {
+                            if (lane_now() == 0)
+                                __hip_atomic_fetch_and(s_rdy + wv, ~gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (got) {
+                                const float4 r = s_pool[threadIdx.x];   // written before its ready bit
+                                p = RMR_MARCH_POINT(L);                 // the request's point (the lane waited)
+                                m = v2(r.x, r.y);
+                                const int kk = __float_as_int(r.w);
+                                npc_apply(P, L, p, (kk << 16) >> 16, kk >> 16, r.z);
+                                waiting = false;
+                            }
+                        }
+                    }
+                }
+                if (act1 && !waiting && !got) {
                     p = RMR_MARCH_POINT(L);
                     F = RMR_PRIM_DIST(L.cw, p, mid, jw);
                     float Fm = F;
@@ -2559,9 +2662,99 @@ RMR_D void trace_main(const KParams& P) {
                     pfin = sum == sum;
                     ok = pfin && (L.cs - delta - npc_eps(P, p) > Fm);
                 }
+                bool done = ok || got;
+                if constexpr (kPool) {
+                    // lanes whose bound failed post their point and cached primitive to the block's pool
+                    const bool fail = act1 && !waiting && !got && !ok;
+                    const uint64_t post = __ballot(fail);
+                    if (post) {
+                        if (fail) s_pool[threadIdx.x] = make_float4(p.x, p.y, p.z, __int_as_float((pfin && F == F) ? L.cw : -1));
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the requests before their bits
+                        if (lane_now() == 0)
+                            __hip_atomic_fetch_or(s_pend + wv, post, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        waiting = waiting || fail;
+                    }
+                    // the lanes served (cache or pool result) step now: their point and map() value are then
+                    // dead while this wave serves the pool
+                    if (done) {
+                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
+                        else march_update<HO, true>(P, L, m, 0, false, p);
+                    }
+                    // serve: when the block holds a batch, or as the cache kernel's wave batch rule (no lane of
+                    // this wave could use the cache, or waiting x R >= 8 x cache-served lanes)
+                    uint64_t pend[4];
+                    int npend = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        pend[j] = rfl64(__hip_atomic_load(s_pend + ((wv + j) & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        npend += __popcll(pend[j]);
+                    }
+                    const int nw = __popcll(__ballot(waiting)), nok = __popcll(__ballot(ok));
+                    const int fr = P.full_threshold >> 8;
+#ifndef RMR_POOL_RATIO
+#define RMR_POOL_RATIO 1
+#endif
+                    if (npend && (npend >= RMR_POOL_SERVE || (nw && (nok == 0 || (RMR_POOL_RATIO && nw * fr >= 8 * nok))))) {
+                        RMR_STAMP(f0);
+                        // claim up to 64 requests: this wave's own first, then the other waves' in turn
+                        uint64_t cl[4];
+                        int tot = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            uint64_t take = tot < 64 ? pend[j] : 0ull;
+                            while (__popcll(take) > 64 - tot) take &= ~(1ull << (63 - __clzll(take)));   // the lowest ones
+                            uint64_t old = 0;
+                            if (take && lane_now() == 0)
+                                old = __hip_atomic_fetch_and(s_pend + ((wv + j) & 3), ~take, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            cl[j] = take ? (rfl64(old) & take) : 0ull;   // (another server may have taken some)
+                            tot += __popcll(cl[j]);
+                        }
+                        // lane t serves the t-th claimed request
+                        const uint32_t t = lane_now();
+                        uint32_t r = t;
+                        uint64_t mw = 0;
+                        int wsel = 0;
+                        bool found = false;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const uint32_t c = (uint32_t)__popcll(cl[j]);
+                            const bool here = !found && r < c;
+                            mw = here ? cl[j] : mw;
+                            wsel = here ? ((wv + j) & 3) : wsel;
+                            r = (!found && !here) ? r - c : r;
+                            found = found || here;
+                        }
+                        if (t < (uint32_t)tot) {
+                            const int id = wsel * 64 + nth_set_bit(mw, r);
+                            const float4 q = s_pool[id];
+                            const V3 sp = v3(q.x, q.y, q.z);
+                            const int ks = __float_as_int(q.w);
+                            float sF = 0.0f, smid = -1.0f;
+                            int sj = 0;
+                            if (ks >= 0) sF = prim_dist_tab(s_dp + kTabStep * ks, sp, smid, sj);   // the owner's F, mid, jw
+                            int kw = -1, kw2 = 0;
+                            float s2 = -__builtin_inff();
+                            const V2 rm = MAP::full(P, sp, kw, kw2, s2, ks, sj, sF, smid, (const float4*)s_dp);
+                            s_pool[id] = make_float4(rm.x, rm.y, s2, __int_as_float((kw & 0xffff) | (kw2 << 16)));
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the results before their bits
+                        if (lane_now() == 0) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                if (cl[j]) __hip_atomic_fetch_or(s_rdy + ((wv + j) & 3), cl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        fulls++;
+#ifdef RMR_PROFILE
+                        RMR_STAMP(f1);
+                        cyc[3] += f1 - f0;
+                        full_lanes += (uint64_t)tot;
+#endif
+                    } else if (RMR_POOL_SLEEP && !__ballot(done)) {
+                        __builtin_amdgcn_s_sleep(1);   // every active lane waits on another wave's batch
+                    }
+                }
                 const uint64_t okm = __ballot(act1 && ok);
-                const uint64_t fm = __ballot(act1 && !ok);
-                bool done = ok;
+                const uint64_t fm = kPool ? 0ull : __ballot(act1 && !ok);
                 const int nf = __popcll(fm), nok = __popcll(okm);
                 const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
@@ -2572,19 +2765,14 @@ RMR_D void trace_main(const KParams& P) {
                         // seeded with the cached primitive only at a finite point: prim_dist's box form
                         // of a sphere drops a NaN coordinate (fmaxf / fminf) where sd_sphere keeps it
                         m = MAP::full(P, p, kw, kw2, s2, (pfin && F == F) ? L.cw : -1, jw, F, mid, RMR_DTAB);
-                        L.cw = kw >= 0 ? kw : 0;
-                        L.cw2 = kw >= 0 ? kw2 : 0;
-                        // |s2| 2^-20: the rounding of the check's own subtractions
-                        L.cs = kw >= 0 ? s2 - fmaf(fabsf(s2), 0x1p-20f, npc_eps(P, p)) -
-                                             (L.phase == PH_NORMAL ? NPC_PROBE_DELTA : 0.0f)
-                                       : -__builtin_inff();
-                        L.cta = L.t;
+                        npc_apply(P, L, p, kw, kw2, s2);
                         done = true;
                     }
                     fulls++;
 #ifdef RMR_PROFILE
                     RMR_STAMP(f1);
                     cyc[3] += f1 - f0;
+                    full_lanes += (uint64_t)nf;
 #endif
                 }
 #ifdef RMR_NPC_CHECK   // diagnostics (RMR_JIT_OPTS=-DRMR_NPC_CHECK): every cached map() against the exact fold
@@ -2597,7 +2785,7 @@ RMR_D void trace_main(const KParams& P) {
                                F, L.cs);
                 }
 #endif
-                if (done) {
+                if (!kPool && done) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO, true>(P, L, m, 0, false, p);
                 }
@@ -2773,7 +2961,10 @@ RMR_D void trace_main(const KParams& P) {
         atomicAdd(P.counters + 4, (unsigned long long)cyc[0]);
         atomicAdd(P.counters + 5, (unsigned long long)cyc[1]);
         atomicAdd(P.counters + 6, (unsigned long long)cyc[2]);
-        if (MAP::kCache) atomicAdd(P.counters + 9, (unsigned long long)cyc[3]);
+        if (MAP::kCache) {
+            atomicAdd(P.counters + 9, (unsigned long long)cyc[3]);
+            atomicAdd(P.counters + 10, (unsigned long long)full_lanes);
+        }
         atomicAdd(P.counters + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
 #endif
     }
