@@ -2215,27 +2215,6 @@ RMR_D void npc_apply(const KParams& P, Lane& L, V3 p, int kw, int kw2, float s2)
     L.cta = L.t;
 }
 
-// the position of the (r + 1)-th lowest set bit of m (r < popcount(m)), per lane: a binary search on
-// the counts of the lower halves (the block pool's request assignment)
-RMR_D int nth_set_bit(uint64_t m, uint32_t r) {
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const uint64_t low = m & ((1ull << w) - 1ull);
-        const uint32_t c = (uint32_t)__popcll(low);
-        const bool up = r >= c;
-        r = up ? r - c : r;
-        m = up ? (m >> w) : low;
-        pos += up ? w : 0;
-    }
-    return pos;
-}
-
-// a 64-bit value made wave-uniform (SGPRs); readfirstlane returns int: through uint32_t, not sign-extended
-RMR_D uint64_t rfl64(uint64_t v) {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
-}
 
 // a defined value the compiler cannot see (no constant to propagate into the loop PHIs): trace_main's
 // lane at kernel entry; the inline asm emits no instruction
@@ -2325,28 +2304,6 @@ static_assert(RMR_QUEUE_PARTS >= 1 && RMR_QUEUE_PARTS <= 64 && RMR_QUEUE_PARTS *
 #ifndef RMR_CHUNK_CACHE
 #define RMR_CHUNK_CACHE 64   // the same for the nearest-primitive cache kernels (6 blocks per CU: 24 KiB of LDS each)
 #endif
-// Block-level pool of the nearest-primitive cache's full map() requests (the hipRTC cache kernels whose
-// primitive table is the compile-time LDS copy, RMR_NPC_TAB_SOA). Without it a wave runs the full map
-// (candidate grid cell + list, or the BVH) for its own lanes whose cache bound failed, once enough of
-// them wait: 28 lanes per batch on average (r06 C4 profile), in batches that take 38% of the waves'
-// cycles. With it a lane whose bound fails posts its point and cached primitive (16 B) to the block's
-// pool in LDS and waits; a wave that serves takes up to 64 requests of any of the block's four waves,
-// runs their full maps 64 wide and posts the results (16 B each) back; the owner lanes pick them up at
-// their next iteration. Only the point and the result move, no path state. The same full map() on the
-// same inputs, so the same bits. The pool's 4 KiB come from 32-unit work chunks (RMR_CHUNK_POOL), so
-// the kernel stays at 6 blocks per CU.
-#ifndef RMR_NPC_POOL
-#define RMR_NPC_POOL 1
-#endif
-#ifndef RMR_CHUNK_POOL
-#define RMR_CHUNK_POOL 32
-#endif
-#ifndef RMR_POOL_SLEEP
-#define RMR_POOL_SLEEP 1
-#endif
-#ifndef RMR_POOL_SERVE
-#define RMR_POOL_SERVE 56   // pending requests in the block at which a wave serves (up to 64 of them)
-#endif
 typedef uint32_t WCount;
 template <int VAR, class MAP, bool PERSIST, bool PROG, class MATS = TableMats>
 RMR_D void trace_main(const KParams& P) {
@@ -2370,9 +2327,7 @@ RMR_D void trace_main(const KParams& P) {
     // per-wave event counters, 32-bit (wave-uniform: SGPRs; 64-bit ones cost the cache kernels
     // scratch round trips), flushed to the 64-bit global counters before any can pass 2^31
     WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, bmaps = 0;
-    constexpr bool kPool = MAP::kCache && HO && RMR_NPC_POOL && RMR_NPC_TAB_SOA;   // RMR_NPC_POOL above
-    constexpr uint32_t CHUNK = MAP::kCache ? (kPool ? RMR_CHUNK_POOL : RMR_CHUNK_CACHE) : RMR_CHUNK;
-    bool waiting = false;   // kPool: this lane's full map() request is in the block's pool
+    constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
     uint32_t rnext = 0, rend = 0;
     // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
@@ -2429,16 +2384,6 @@ RMR_D void trace_main(const KParams& P) {
     __shared__ float s_cold[kStash ? kColdWords : 1][kStash ? 256 : 1];
     // the cached primitives' table in LDS (per-lane reads of the cache path)
     __shared__ float4 s_dp[MAP::kCache ? 2 * RMR_NPC_LDS_MAX : 1];
-    // kPool: one request / result slot per lane of the block (p.xyz, seed leaf index | m.x, m.y, s2,
-    // kw | kw2 << 16) and, per wave, the bits of its lanes whose request is pending / result is ready
-    __shared__ float4 s_pool[kPool ? 256 : 1];
-    __shared__ unsigned long long s_pend[kPool ? 4 : 1], s_rdy[kPool ? 4 : 1];
-    if constexpr (kPool) {
-        if (threadIdx.x < 4) {
-            s_pend[threadIdx.x] = 0ull;
-            s_rdy[threadIdx.x] = 0ull;
-        }
-    }
     // the stepped Mandelbulb kernel (8 waves / SIMD, 20 KiB of LDS per block): the RNG state (seeds
     // gx + time, gy + time and the chain value randChange), which only shading reads and advances,
     // waits in LDS between shading batches instead of in registers the allocator spilled to scratch
@@ -2605,27 +2550,7 @@ RMR_D void trace_main(const KParams& P) {
                 float F = 0.0f, mid = -1.0f;
                 int jw = 0;
                 bool pfin = false;   // a point without NaN (and without +-inf of both signs)
-                bool got = false;    // kPool: this lane's full map() result came back from the block's pool
-                if constexpr (kPool) {
-                    if (__ballot(waiting)) {
-                        const uint64_t rdy = rfl64(__hip_atomic_load(s_rdy + wv, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-                        got = waiting && ((rdy >> lane_now()) & 1ull) != 0;
-                        const uint64_t gm = __ballot(got);
-                        if (gm) {
-                            if (lane_now() == 0)
-                                __hip_atomic_fetch_and(s_rdy + wv, ~gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if (got) {
-                                const float4 r = s_pool[threadIdx.x];   // written before its ready bit
-                                p = RMR_MARCH_POINT(L);                 // the request's point (the lane waited)
-                                m = v2(r.x, r.y);
-                                const int kk = __float_as_int(r.w);
-                                npc_apply(P, L, p, (kk << 16) >> 16, kk >> 16, r.z);
-                                waiting = false;
-                            }
-                        }
-                    }
-                }
-                if (act1 && !waiting && !got) {
+                if (act1) {
                     p = RMR_MARCH_POINT(L);
                     F = RMR_PRIM_DIST(L.cw, p, mid, jw);
                     float Fm = F;
@@ -2662,99 +2587,9 @@ RMR_D void trace_main(const KParams& P) {
                     pfin = sum == sum;
                     ok = pfin && (L.cs - delta - npc_eps(P, p) > Fm);
                 }
-                bool done = ok || got;
-                if constexpr (kPool) {
-                    // lanes whose bound failed post their point and cached primitive to the block's pool
-                    const bool fail = act1 && !waiting && !got && !ok;
-                    const uint64_t post = __ballot(fail);
-                    if (post) {
-                        if (fail) s_pool[threadIdx.x] = make_float4(p.x, p.y, p.z, __int_as_float((pfin && F == F) ? L.cw : -1));
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the requests before their bits
-                        if (lane_now() == 0)
-                            __hip_atomic_fetch_or(s_pend + wv, post, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        waiting = waiting || fail;
-                    }
-                    // the lanes served (cache or pool result) step now: their point and map() value are then
-                    // dead while this wave serves the pool
-                    if (done) {
-                        if (L.phase == PH_NORMAL) normal_update(L, m.x);
-                        else march_update<HO, true>(P, L, m, 0, false, p);
-                    }
-                    // serve: when the block holds a batch, or as the cache kernel's wave batch rule (no lane of
-                    // this wave could use the cache, or waiting x R >= 8 x cache-served lanes)
-                    uint64_t pend[4];
-                    int npend = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        pend[j] = rfl64(__hip_atomic_load(s_pend + ((wv + j) & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                        npend += __popcll(pend[j]);
-                    }
-                    const int nw = __popcll(__ballot(waiting)), nok = __popcll(__ballot(ok));
-                    const int fr = P.full_threshold >> 8;
-#ifndef RMR_POOL_RATIO
-#define RMR_POOL_RATIO 1
-#endif
-                    if (npend && (npend >= RMR_POOL_SERVE || (nw && (nok == 0 || (RMR_POOL_RATIO && nw * fr >= 8 * nok))))) {
-                        RMR_STAMP(f0);
-                        // claim up to 64 requests: this wave's own first, then the other waves' in turn
-                        uint64_t cl[4];
-                        int tot = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            uint64_t take = tot < 64 ? pend[j] : 0ull;
-                            while (__popcll(take) > 64 - tot) take &= ~(1ull << (63 - __clzll(take)));   // the lowest ones
-                            uint64_t old = 0;
-                            if (take && lane_now() == 0)
-                                old = __hip_atomic_fetch_and(s_pend + ((wv + j) & 3), ~take, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            cl[j] = take ? (rfl64(old) & take) : 0ull;   // (another server may have taken some)
-                            tot += __popcll(cl[j]);
-                        }
-                        // lane t serves the t-th claimed request
-                        const uint32_t t = lane_now();
-                        uint32_t r = t;
-                        uint64_t mw = 0;
-                        int wsel = 0;
-                        bool found = false;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const uint32_t c = (uint32_t)__popcll(cl[j]);
-                            const bool here = !found && r < c;
-                            mw = here ? cl[j] : mw;
-                            wsel = here ? ((wv + j) & 3) : wsel;
-                            r = (!found && !here) ? r - c : r;
-                            found = found || here;
-                        }
-                        if (t < (uint32_t)tot) {
-                            const int id = wsel * 64 + nth_set_bit(mw, r);
-                            const float4 q = s_pool[id];
-                            const V3 sp = v3(q.x, q.y, q.z);
-                            const int ks = __float_as_int(q.w);
-                            float sF = 0.0f, smid = -1.0f;
-                            int sj = 0;
-                            if (ks >= 0) sF = prim_dist_tab(s_dp + kTabStep * ks, sp, smid, sj);   // the owner's F, mid, jw
-                            int kw = -1, kw2 = 0;
-                            float s2 = -__builtin_inff();
-                            const V2 rm = MAP::full(P, sp, kw, kw2, s2, ks, sj, sF, smid, (const float4*)s_dp);
-                            s_pool[id] = make_float4(rm.x, rm.y, s2, __int_as_float((kw & 0xffff) | (kw2 << 16)));
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the results before their bits
-                        if (lane_now() == 0) {
-#pragma unroll
-                            for (int j = 0; j < 4; j++)
-                                if (cl[j]) __hip_atomic_fetch_or(s_rdy + ((wv + j) & 3), cl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                        fulls++;
-#ifdef RMR_PROFILE
-                        RMR_STAMP(f1);
-                        cyc[3] += f1 - f0;
-                        full_lanes += (uint64_t)tot;
-#endif
-                    } else if (RMR_POOL_SLEEP && !__ballot(done)) {
-                        __builtin_amdgcn_s_sleep(1);   // every active lane waits on another wave's batch
-                    }
-                }
                 const uint64_t okm = __ballot(act1 && ok);
-                const uint64_t fm = kPool ? 0ull : __ballot(act1 && !ok);
+                const uint64_t fm = __ballot(act1 && !ok);
+                bool done = ok;
                 const int nf = __popcll(fm), nok = __popcll(okm);
                 const int ft = P.full_threshold & 0xff, fr = P.full_threshold >> 8;
                 if (fm && (okm == 0 || nf >= ft || nf * fr >= 8 * nok)) {
@@ -2785,7 +2620,7 @@ RMR_D void trace_main(const KParams& P) {
                                F, L.cs);
                 }
 #endif
-                if (!kPool && done) {
+                if (done) {
                     if (L.phase == PH_NORMAL) normal_update(L, m.x);
                     else march_update<HO, true>(P, L, m, 0, false, p);
                 }

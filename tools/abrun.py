@@ -141,6 +141,8 @@ def main():
                 c, tot = cnt[i], max(1, cnt[i][7])
                 out[v["label"]]["sections"] = {"refill": round(c[4] / tot, 4), "map_loop": round(c[5] / tot, 4),
                                                "shade": round(c[6] / tot, 4), "cache_full_maps": round(c[9] / tot, 4)}
+                if c[3]:   # cache kernels: lanes per full map() batch (counter 10 of the profiling build)
+                    out[v["label"]]["lanes_per_full_batch"] = round(c[10] / c[3], 2)
         print(json.dumps(out), flush=True)
     for r in ctx:
         r.close()
