@@ -3,8 +3,9 @@ sample (Program.cpp:184-284), with the library's call batching (rmr_set_call_bat
 
 Batched calls must give the bits of the same calls made one launch each, and of the oracle: every
 pixel's samples, seeds and running-mean order are the same whatever launch carries them. The tile
-grids here do not divide into 8x8 tiles (per-tile clipping, rmr_api.cpp tile_at), and the calls
-interleave with the entry points that flush them."""
+grids here do not divide into 8x8 tiles (a held set of rects goes out as one launch over their
+bounding box when they fill it, rmr_api.cpp flush_calls), and the calls interleave with the entry
+points that flush them."""
 import os
 
 import numpy as np
@@ -129,3 +130,25 @@ def test_call_batching_is_off_on_a_caller_stream_and_reports_errors_at_the_call(
         assert (acc[..., 3] == 1.0).all().item()
     finally:
         r.close()
+
+
+def test_tile_list_cache_eviction_keeps_results(renderer):
+    """More distinct tile lists than the context caches (rmr_api.cpp kTileCacheEntries = 64): the least
+    recently used device lists are freed after a stream sync and uploaded again when reused. One launch per
+    call (batching off), so every call is its own tile list; the image equals one batched render."""
+    W, H = 80, 72
+    prm, view = _setup(renderer, CORNELL, "rm1", W, H, {"max_bounces": 1})
+    times = time_schedule(2, frame=4)
+    rects = [((x, y), (x + 8, y + 8)) for y in range(0, H, 8) for x in range(0, W, 8)]   # 90 rects
+    assert len(rects) > 64
+    try:
+        renderer.set_call_batching(0)
+        renderer.reload()
+        for s in range(2):   # the second pass reuses lists evicted during the first
+            for mn, mx in rects:
+                renderer.render(float(times[s]), mn, mx, s)
+        got = renderer.read_accum()
+    finally:
+        renderer.set_call_batching(-1)
+    cpu = oracle.Oracle(_tables(CORNELL, "rm1"), prm, view, W, H).render(times)
+    assert same_bits(got, cpu).all()
