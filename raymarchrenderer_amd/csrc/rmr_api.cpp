@@ -131,6 +131,7 @@ struct rmr_ctx {
     int instrument = 0;   // RMR_INSTR_* (rmr_set_instrument): instrumented specialised kernels
     int grid_per_cu = 0;  // 0 = occupancy
     int grid_reserve = 0;  // persistent grid: workgroups left free of the occupancy grid (rmr_set_grid_reserve)
+    int small_chunk = 64;  // fewest units per work claim when a launch is too small to fill every wave (0: off)
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
     // 1-spp frame is 65536 units and runs 0.157 -> 0.106 ms per launch specialised (the compile,
@@ -387,6 +388,7 @@ int upload_scene(rmr_ctx* c) {
         c->full_threshold = (c->full_threshold & ~0xff) | std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = RMR_ENV("RMR_FULL_R"))
         c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
+    if (const char* e = RMR_ENV("RMR_SMALL_CHUNK")) c->small_chunk = std::max(0, std::atoi(e));
     c->scene_loaded = true;
     c->jit_ready = false;
     c->jit_failed = false;
@@ -927,11 +929,23 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         // 256x256 1-spp launch (C1) on the full grid: 0.47 ms, almost all of it waves that find no
         // work; the per-path kernel takes one wave per 64 units as it is). Waves per block and units
         // per chunk of the kernel that runs.
+        // A launch with less work than one chunk per wave of the grid (a tile of one sample: the
+        // reference's Graphics::Render call) takes smaller claims instead, down to small_chunk units,
+        // so its paths spread over more CUs rather than running after one another in a few waves.
+        // 480x270 tiles of one sample, same process (r06m_small_chunk.log), 64 against 128 units:
+        // Cornell-5 -21%, RM3 -7%, Mandelbulb -18%; 32 / 16 slower again. Single-bounce paths are too
+        // short for it (C1's 256x256 frame +6%): those launches keep the kernel's chunk.
         int grid = full_grid;
+        P.chunk_units = 0;
         if (c->kernel_mode == 0 && c->grid_per_cu <= 0) {
-            const uint64_t per_block = (uint64_t)((use_jit ? c->jit.block : 256) / 64) * (use_jit ? c->jit.chunk : 128);
-            const uint64_t want = (P.n_units + per_block - 1) / per_block;
-            grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, full_grid - c->grid_reserve), want));
+            const uint64_t wpb = (uint64_t)((use_jit ? c->jit.block : 256) / 64), kchunk = use_jit ? c->jit.chunk : 128;
+            const uint64_t avail = (uint64_t)std::max(1, full_grid - c->grid_reserve);
+            uint64_t ck = kchunk;
+            if (c->small_chunk > 0 && P.max_bounces >= 2 && P.n_units < avail * wpb * kchunk)
+                ck = std::min(kchunk, std::max<uint64_t>((uint64_t)c->small_chunk, (P.n_units + avail * wpb - 1) / (avail * wpb)));
+            if (ck < kchunk) P.chunk_units = (uint32_t)ck;
+            const uint64_t want = (P.n_units + wpb * ck - 1) / (wpb * ck);
+            grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(avail, want));
         }
         // tuned shading batch size of the kernel that runs (measured: C2 +2% at 20; the Mandelbulb
         // and the cached BVH map -1..2%)

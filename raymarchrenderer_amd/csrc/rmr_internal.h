@@ -121,6 +121,8 @@ struct KParams {
     const float* times;         // [nspp] rand() seed per sample (null when nspp == 1: time1)
     float time1;                // the seed of a one-sample launch, as a kernel argument (no copy)
     uint64_t n_units;           // nspp * n_tiles * 64
+    uint32_t chunk_units;       // units a wave takes per claim (0: the kernel's chunk; smaller for small
+                                // launches, so they spread over every CU, rmr_api.cpp render_tiles)
     float4* samp;               // [nspp][n_tiles][64] per-sample radiance
     float4* accum;              // W*H running mean
     unsigned long long* queue;  // persistent work counters (kQueueBytes: one per partition, 128 B apart)

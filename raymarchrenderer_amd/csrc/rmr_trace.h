@@ -2329,6 +2329,8 @@ RMR_D void trace_main(const KParams& P) {
     WCount maps = 0, iters = 0, shades = 0, fulls = 0, shaded = 0, bmaps = 0;
     constexpr uint32_t CHUNK = MAP::kCache ? RMR_CHUNK_CACHE : RMR_CHUNK;
     const uint32_t n_units = (uint32_t)P.n_units;   // < 2^32 per launch (host chunking)
+    // units per claim: the LDS ray buffer's CHUNK, or fewer for a small launch (the host's chunk_units)
+    const uint32_t CK = P.chunk_units - 1u < CHUNK ? P.chunk_units : CHUNK;
     uint32_t rnext = 0, rend = 0;
     // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
     // apart): a wave starts on partition blockIdx % parts (with 8 or 16 partitions, blocks of one XCD
@@ -2337,9 +2339,9 @@ RMR_D void trace_main(const KParams& P) {
     // short paths fetch ~80 chunks per microsecond, and one counter held its 1080p 16-spp frame at
     // 3.24 ms against 0.98 / 0.97 ms with 8 / 16 partitions (round 4; Cornell-5, RM3,
     // multilight, the Mandelbulb 1-2.5% faster with 16 than with one counter).
-    const uint32_t n_chunks = (n_units + CHUNK - 1) / CHUNK;
+    const uint32_t n_chunks = (n_units + CK - 1) / CK;
     auto part_begin = [&](uint32_t q) -> uint32_t {   // first unit of partition q (q = parts: the end)
-        return (uint32_t)(((uint64_t)n_chunks * q) / (uint32_t)RMR_QUEUE_PARTS) * CHUNK;
+        return (uint32_t)(((uint64_t)n_chunks * q) / (uint32_t)RMR_QUEUE_PARTS) * CK;
     };
     uint32_t part = blockIdx.x % (uint32_t)RMR_QUEUE_PARTS, tried = 0;
     // small launches (fewer than 4 chunks per wave of the grid: C1's 256 x 256 frame) scan the counters
@@ -2434,11 +2436,11 @@ RMR_D void trace_main(const KParams& P) {
                     for (;;) {
                         const uint32_t pb = part_begin(part), pe = part_begin(part + 1);
                         unsigned int off = 0;
-                        if (lane_now() == 0) off = atomicAdd((unsigned int*)P.queue + RMR_QUEUE_STRIDE * part, CHUNK);
+                        if (lane_now() == 0) off = atomicAdd((unsigned int*)P.queue + RMR_QUEUE_STRIDE * part, CK);
                         off = __builtin_amdgcn_readfirstlane(off);
                         if (off < pe - pb) {
                             base = pb + off;
-                            rend = n_units - base > CHUNK ? base + CHUNK : n_units;
+                            rend = n_units - base > CK ? base + CK : n_units;
                             break;
                         }
                         // the next few partitions in turn (one atomic each), then a scan of all counters
@@ -2480,7 +2482,7 @@ RMR_D void trace_main(const KParams& P) {
 #endif
                     if (!exhausted) {  // the chunk's primary rays, all 64 lanes at once
                         chunk_base = base;
-                        for (uint32_t sl = lane_now(); sl < CHUNK; sl += 64) {
+                        for (uint32_t sl = lane_now(); sl < CK; sl += 64) {
                             if (base + sl < rend) s_ray[wv][sl] = chunk_ray<HO>(P, base + sl);
                         }
                         __builtin_amdgcn_wave_barrier();

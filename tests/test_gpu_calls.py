@@ -152,3 +152,29 @@ def test_tile_list_cache_eviction_keeps_results(renderer):
         renderer.set_call_batching(-1)
     cpu = oracle.Oracle(_tables(CORNELL, "rm1"), prm, view, W, H).render(times)
     assert same_bits(got, cpu).all()
+
+
+def test_small_launch_claims_keep_results(monkeypatch):
+    """A launch smaller than one chunk per wave of the grid takes 64-unit claims over more waves
+    (rmr_api.cpp render_tiles, small_chunk); the diagnostic library's RMR_SMALL_CHUNK=0 keeps the
+    kernel's chunk. A one-sample 480x270 tile (a Graphics::Render call of the 4x4 grid at 1080p) and a
+    one-sample 30x20 rect give the same bits either way, and the oracle's."""
+    W, H = 480, 270
+    out = {}
+    for mode in ("0", "64", "16"):
+        monkeypatch.setenv("RMR_SMALL_CHUNK", mode)
+        r = Renderer(0, W, H, diag=True)
+        try:
+            prm, view = _setup(r, CORNELL, "rm1", W, H, {"max_bounces": 3})
+            times = time_schedule(2, frame=5)
+            r.set_call_batching(0)
+            r.render(float(times[0]), (0, 0), (W, H), 0)
+            r.render(float(times[1]), (7, 3), (37, 23), 1)
+            out[mode] = r.read_accum()
+        finally:
+            r.close()
+    assert same_bits(out["0"], out["64"]).all() and same_bits(out["0"], out["16"]).all()
+    o = oracle.Oracle(_tables(CORNELL, "rm1"), prm, view, W, H)
+    acc = o.render([times[0]], rect=(0, 0, 48, 40))   # a corner of the first call's tile
+    acc = o.render([times[1]], rect=(7, 3, 37, 23), first_sample=1, accum=acc)
+    assert same_bits(out["64"][:40, :48], acc[:40, :48]).all()

@@ -43,6 +43,10 @@ CASES = {
     "multilight": (os.path.join(G, "multilight.scene"), "rm1", 16, 1920, 1080, 16),
     "csg64": (os.path.join(S, "csg64.scene"), "rm1", 4, 1920, 1080, 8),
     "csg_nodes": (os.path.join(S, "csg_nodes.scene"), "rm1", 4, 1920, 1080, 8),
+    # one tile of the reference's 4x4 grid at 1080p, one sample: a Graphics::Render call's launch
+    "c2t": (os.path.join(S, "cornell5.scene"), "rm1", 4, 480, 270, 1),
+    "rm3t": (None, "rm3", 16, 480, 270, 1),
+    "c3t": (os.path.join(S, "mandelbulb.scene"), "rm1", 2, 480, 270, 1),
 }
 
 
