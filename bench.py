@@ -400,9 +400,25 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # a rank that fails (e.g. its rendezvous port was taken between free_port and the bind) would leave
+    # the others waiting in the rendezvous: end them (the processes started here, by PID)
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc is not None and rc != 0]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc is not None for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 class _StagedDist:
