@@ -131,6 +131,7 @@ struct rmr_ctx {
     int instrument = 0;   // RMR_INSTR_* (rmr_set_instrument): instrumented specialised kernels
     int grid_per_cu = 0;  // 0 = occupancy
     int grid_reserve = 0;  // persistent grid: workgroups left free of the occupancy grid (rmr_set_grid_reserve)
+    bool diag_no_fold = false;   // RMR_DIAG_NO_FOLD (diagnostic library, timing only): no k_fold launch
     int small_chunk = 64;  // fewest units per work claim when a launch is too small to fill every wave (0: off)
     // hipRTC per-scene specialisation (rmr_jit.hpp): 0 off, 1 always, 2 auto (launches of
     // >= jit_min_units units; smaller renders use the ahead-of-time kernels). 2^16: C1's 256x256
@@ -389,6 +390,8 @@ int upload_scene(rmr_ctx* c) {
     if (const char* e = RMR_ENV("RMR_FULL_R"))
         c->full_threshold = (c->full_threshold & 0xff) | (std::max(0, std::min(255, std::atoi(e))) << 8);
     if (const char* e = RMR_ENV("RMR_SMALL_CHUNK")) c->small_chunk = std::max(0, std::atoi(e));
+    c->diag_no_fold = false;
+    if (const char* e = RMR_ENV("RMR_DIAG_NO_FOLD")) c->diag_no_fold = std::atoi(e) != 0;
     c->scene_loaded = true;
     c->jit_ready = false;
     c->jit_failed = false;
@@ -966,8 +969,12 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
             HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
         }
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
-        HIPCHK(c, rmr::launch_fold(P, c->stream));
-        c->queue_dirty = false;
+        // (RMR_DIAG_NO_FOLD: what the fold costs the frame, a timing experiment with a wrong accumulator;
+        // the next launch then zeroes the queue with a memset)
+        if (!c->diag_no_fold) {
+            HIPCHK(c, rmr::launch_fold(P, c->stream));
+            c->queue_dirty = false;
+        }
         HIPCHK(c, hipEventRecord(ev.c, c->stream));
         c->pending.push_back(ev);
         c->stats.trace_launches++;
