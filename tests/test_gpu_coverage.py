@@ -5,7 +5,7 @@
   schedule time(f, s) = 1000 f + 0.016 s, bitwise against the oracle at frames 1, 37 and 90;
 * sample-plane chunking (rmr_api.cpp render_tiles: launches split at the sample-plane budget) —
   several launches per frame fold to the same bits as one;
-* the full C2, C3, C4 and C5 frames (1920x1080; C4 3840x2160) through the multi-GPU tile path,
+* the full C2, C3, C4, C5, RM2 and RM3 frames (1920x1080; C4 3840x2160) through the multi-GPU tile path,
   checked by properties that do not depend on size (finite, non-negative, alpha 1) and bitwise
   against the oracle on random 8x8 tiles;
 * FrameRenderer's stream ordering (zero -> render -> collective on one stream) read back on that
@@ -21,7 +21,7 @@ import pytest
 from oracle import camera, oracle, scene_compile
 from raymarchrenderer_amd import RMRError, abi, time_schedule
 
-from .conftest import SCENES
+from .conftest import GOLDEN, SCENES
 
 pytestmark = pytest.mark.gpu
 
@@ -40,10 +40,13 @@ def _c5_scene(frame):
     return sc
 
 
-def _setup(r, scene, W, H, **kw):
+def _setup(r, scene, W, H, variant="rm1", **kw):
     r.set_image_size(W, H)
     r.reload()
-    r.load_scene(scene, "rm1")
+    if scene is None:
+        r.load_builtin(variant)
+    else:
+        r.load_scene(scene, variant)
     prm = abi.default_params(**kw)
     r.set_params(prm)
     view = camera.default_view(W, H)
@@ -130,13 +133,13 @@ def test_full_c2_frame_properties_and_sampled_tiles(renderer):
 
 
 def _full_frame_check(renderer, scene, W, H, spp, bounces, frame=0, ntiles=6, seed=11,
-                      mean_range=(0.0, 10.0)):
+                      mean_range=(0.0, 10.0), variant="rm1"):
     """Render a BASELINE config's full frame through rmr_render_tiles (32x32 tiles, the bench's
     path: the specialised kernel rmr_jit_trace), then check size-independent properties (finite,
     non-negative, alpha 1, a plausible frame mean) and `ntiles` random 8x8 tiles bitwise against
     the oracle (RM1:567-613 per pixel)."""
     from raymarchrenderer_amd.multi_gpu import frame_tiles
-    prm, view = _setup(renderer, scene, W, H, max_bounces=bounces)
+    prm, view = _setup(renderer, scene, W, H, variant=variant, max_bounces=bounces)
     times = time_schedule(spp, frame=frame)
     renderer.reset_stats()
     renderer.render_tiles(times, frame_tiles(W, H, 32), 32)
@@ -147,8 +150,10 @@ def _full_frame_check(renderer, scene, W, H, spp, bounces, frame=0, ntiles=6, se
     assert (img[..., :3] >= 0).all() and (img[..., 3] == 1.0).all()
     m = float(img[..., :3].mean())
     assert mean_range[0] < m < mean_range[1], m
-    tables = scene_compile.compile_scene(scene, "rm1") if isinstance(scene, dict) else \
-        scene_compile.load_scene_file(scene, "rm1")
+    if scene is None or isinstance(scene, dict):
+        tables = scene_compile.compile_scene(scene or {}, variant)
+    else:
+        tables = scene_compile.load_scene_file(scene, variant)
     orc = oracle.Oracle(tables, prm, view, W, H)
     rng = np.random.default_rng(seed)
     picks = [(int(rng.integers(0, W // 8)) * 8, int(rng.integers(0, H // 8)) * 8) for _ in range(ntiles)]
@@ -227,6 +232,19 @@ def test_full_c5_frame_properties_and_sampled_tiles(renderer):
     renderer.render_tiles(time_schedule(1, frame=0), frame_tiles(1920, 1080, 32), 32)
     _full_frame_check(renderer, _c5_scene(37), 1920, 1080, 2, 4, frame=37, ntiles=6, seed=53,
                       mean_range=(0.05, 1.0))
+
+
+def test_full_rm3_frame_properties_and_sampled_tiles(renderer):
+    """RM3 as the reference wires it (Graphics.cpp:272; bench config rm3): the built-in scene at
+    1920x1080, 16 bounces, spectral paths; 1 spp instead of 4."""
+    _full_frame_check(renderer, None, 1920, 1080, 1, 16, ntiles=6, seed=61, mean_range=(0.0, 10.0),
+                      variant="rm3")
+
+
+def test_full_rm2_frame_properties_and_sampled_tiles(renderer):
+    """RM2 (bench config rm2): simple.scene at 1920x1080, 16 bounces; 1 spp instead of 4."""
+    _full_frame_check(renderer, os.path.join(GOLDEN, "scenes", "simple.scene"), 1920, 1080, 1, 16,
+                      ntiles=6, seed=67, mean_range=(0.0, 10.0), variant="rm2")
 
 
 def test_frame_renderer_stream_ordering_without_device_sync():
