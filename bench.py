@@ -144,6 +144,9 @@ def parse():
     ap.add_argument("--call-batching", type=int, default=-1, choices=[-1, 0, 1],
                     help="--api render: rmr_set_call_batching (-1 auto = on for a context that owns its stream, "
                          "the default; 0: one launch per call)")
+    ap.add_argument("--launch-streams", type=int, default=-1,
+                    help="rmr_set_launch_streams for every renderer context (-1: the library default; 0 off; "
+                         "N >= 2: consecutive trace launches overlap on N private streams)")
     return ap.parse_args()
 
 
@@ -555,6 +558,7 @@ def predict_partition(args, cfg):
 
     def timed(tile, rank, world, nspp):
         fr = FrameRenderer(rs, accs, W, H, tile, rank, world, None, streams=streams,
+                           launch_streams=args.launch_streams if args.launch_streams >= 0 else None,
                            grid_reserve=args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE)
         if args.tile_order != "rows":
             if tile not in cost_maps:
@@ -637,6 +641,8 @@ def api_render_bench(args, cfg):
     load_into(r, cfg, scene_for_frame(cfg, 0))
     r.set_params(abi.default_params(max_bounces=cfg["bounces"]))
     r.set_call_batching(args.call_batching)
+    if args.launch_streams >= 0:
+        r.set_launch_streams(args.launch_streams)
     rects = [((x * cw, y * ch), ((x + 1) * cw, (y + 1) * ch)) for x, y in order]
 
     def frame():
@@ -683,6 +689,7 @@ def api_render_bench(args, cfg):
                                   "(Program.cpp fixed-spp loop)" % (cfg["name"], W, H, spp, cfg["bounces"]),
                       "config": args.config, "api": "render", "grid": "%dx%d" % (gw, gh), "tile_px": [cw, ch],
                       "order": "spiral (Program.cpp:203-222)", "call_batching": args.call_batching,
+                      "launch_streams": r.launch_streams,
                       "width": W, "height": H, "spp": spp,
                       "max_bounces": cfg["bounces"]},
            "calls": {"per_step": len(rects) * spp, "per_s": round(calls / elapsed, 1),
@@ -839,6 +846,7 @@ def main():
     torch.cuda.synchronize()
     reserve = args.grid_reserve if args.grid_reserve >= 0 else OVERLAP_GRID_RESERVE
     fr = FrameRenderer(rs, accs, W, H, TILE, rank, world, dist if dist_on else None, streams=streams,
+                       launch_streams=args.launch_streams if args.launch_streams >= 0 else None,
                        grid_reserve=reserve)
     static_times = time_schedule(spp)
     # cost order where the tiles' costs are uneven and trial frames in both orders say it is faster
@@ -1004,7 +1012,8 @@ def main():
                           "samples_per_step": W * H * spp, "tile": TILE, "tile_order": "cost" if tiles_reordered else "rows",
                           "tile_order_trial_ms": getattr(fr, "tile_order_trial_ms", None),
                           "parallelism": "tiles%d" % world,
-                          "frame_streams": n_ctx, "grid_reserve": reserve if n_ctx > 1 else 0},
+                          "frame_streams": n_ctx, "grid_reserve": reserve if n_ctx > 1 else 0,
+                          "launch_streams": rs[0].launch_streams},
                "roofline": roof, "cpu_baseline": cpu, "psnr_vs_reference": parity,
                "reference_equivalent_work": work_ref}
         if dist_on:

@@ -41,6 +41,8 @@ using rmr::TileXY;
 
 struct EventPair { hipEvent_t a, b, c; };
 
+constexpr int kSlotGridReserve = 32;   // workgroups a slotted launch leaves free for the previous fold
+
 struct rmr_ctx {
     int device = 0;
     int n_cu = 256;
@@ -91,6 +93,27 @@ struct rmr_ctx {
     bool accum_external = false;
     float4* d_samp = nullptr;
     size_t samp_cap = 0;
+    // Launch slots (rmr_set_launch_streams): trace launches go round-robin to private streams, each with
+    // its own sample planes and work queue, so a launch's drain (its last long paths on a nearly idle
+    // chip) overlaps the next launch's start. Every fold stays on the context's stream, after its trace's
+    // `done` event, in call order: a sync of the context's stream covers every trace queued before it,
+    // and the accumulator sees the same running-mean order. A slot's planes and queue are reused once
+    // the fold that read them (`freed`) is done.
+    struct Slot {
+        hipStream_t s = nullptr;
+        float4* samp = nullptr;
+        size_t cap = 0;
+        unsigned long long* queue = nullptr;
+        bool queue_dirty = true;
+        hipEvent_t done = nullptr, freed = nullptr;
+        bool in_use = false;
+    };
+    std::vector<Slot> slots;
+    int launch_streams = 2;       // fewer than 2: every launch on the context's stream
+    int slot_reserve = kSlotGridReserve;   // workgroups a slotted launch leaves free (RMR_SLOT_RESERVE)
+    size_t next_slot = 0;
+    float4* last_samp = nullptr;  // the last launch's planes (rmr_trace_samples)
+    hipEvent_t trace_end = nullptr;   // after the last trace launch, on its stream
     // device tile lists by content (tile_list): a list is uploaded once and reused by every later launch
     // with the same tiles (the reference's per-tile, per-sample calls; a rank's share each frame) with no
     // copy and no stream sync; least recently used entries go beyond kTileCacheEntries
@@ -348,6 +371,8 @@ bool any_program(const std::vector<rmr::DMat>& dm) {
     return false;
 }
 
+int free_slots(rmr_ctx* c);
+
 int upload_scene(rmr_ctx* c) {
     const CompiledScene& s = c->scene;
     int r;
@@ -392,6 +417,11 @@ int upload_scene(rmr_ctx* c) {
     if (const char* e = RMR_ENV("RMR_SMALL_CHUNK")) c->small_chunk = std::max(0, std::atoi(e));
     c->diag_no_fold = false;
     if (const char* e = RMR_ENV("RMR_DIAG_NO_FOLD")) c->diag_no_fold = std::atoi(e) != 0;
+    if (const char* e = RMR_ENV("RMR_SLOT_RESERVE")) c->slot_reserve = std::max(0, std::atoi(e));
+    if (const char* e = RMR_ENV("RMR_LAUNCH_STREAMS")) {   // (experiments; the slots go at the next launch)
+        (void)free_slots(c);
+        c->launch_streams = std::max(0, std::min(4, std::atoi(e)));
+    }
     c->scene_loaded = true;
     c->jit_ready = false;
     c->jit_failed = false;
@@ -679,6 +709,74 @@ int ensure_samp(rmr_ctx* c, size_t n) {
     return RMR_OK;
 }
 
+
+// Create every launch slot's stream, events and work queue (rmr_create, rmr_set_launch_streams: a
+// stream created at a slot's first launch cost that launch ~6 ms, r06s_timeline_full_ls2.txt).
+int make_slots(rmr_ctx* c) {
+    c->slots.resize(c->launch_streams >= 2 ? (size_t)c->launch_streams : 0);
+    c->next_slot = 0;
+    for (auto& S : c->slots) {
+        if (S.s) continue;
+        HIPCHK(c, hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&S.freed, hipEventDisableTiming));
+        HIPCHK(c, hipMalloc((void**)&S.queue, rmr::kQueueBytes));
+        S.queue_dirty = true;
+    }
+    return RMR_OK;
+}
+
+// The next launch slot, for `units` sample-plane entries. Planes grow for every slot at once (the
+// launches that follow are the same size: no allocation inside a run of them), each once the fold
+// that last read it is done; the slot's stream then waits for that fold.
+int slot_prepare(rmr_ctx* c, size_t units, rmr_ctx::Slot** out) {
+    int r;
+    if (c->slots.empty() || !c->slots[0].s) {
+        if ((r = make_slots(c))) return r;
+    }
+    if (units > c->slots[c->next_slot].cap) {
+        for (auto& T : c->slots) {
+            if (units <= T.cap) continue;
+            if (T.samp) {
+                if (T.in_use) HIPCHK(c, hipEventSynchronize(T.freed));
+                (void)hipFree(T.samp);
+                T.samp = nullptr;
+                T.cap = 0;
+            }
+            HIPCHK(c, hipMalloc((void**)&T.samp, units * sizeof(float4)));
+            T.cap = units;
+        }
+    }
+    rmr_ctx::Slot& S = c->slots[c->next_slot];
+    c->next_slot = (c->next_slot + 1) % c->slots.size();
+    if (S.in_use) HIPCHK(c, hipStreamWaitEvent(S.s, S.freed, 0));
+    *out = &S;
+    return RMR_OK;
+}
+
+// Release the launch slots (the context's stream synced first: every trace queued is done).
+int free_slots(rmr_ctx* c) {
+    if (c->slots.empty() && !c->trace_end) return RMR_OK;
+    const hipError_t e = c->stream ? hipStreamSynchronize(c->stream) : hipSuccess;
+    for (auto& S : c->slots) {
+        if (S.s) {
+            (void)hipStreamSynchronize(S.s);
+            (void)hipStreamDestroy(S.s);
+        }
+        if (S.done) (void)hipEventDestroy(S.done);
+        if (S.freed) (void)hipEventDestroy(S.freed);
+        if (S.samp) (void)hipFree(S.samp);
+        if (S.queue) (void)hipFree(S.queue);
+    }
+    c->slots.clear();
+    c->next_slot = 0;
+    if (c->trace_end) (void)hipEventDestroy(c->trace_end);
+    c->trace_end = nullptr;
+    c->last_samp = c->d_samp;
+    if (e != hipSuccess) return fail(c, RMR_E_HIP, std::string("launch slots: ") + hipGetErrorString(e));
+    return RMR_OK;
+}
+
 constexpr size_t kTileCacheEntries = 64;
 
 uint64_t tiles_hash(const std::vector<TileXY>& t) {
@@ -721,7 +819,8 @@ int tile_list(rmr_ctx* c, const std::vector<TileXY>& t, const TileXY** out) {
 }
 
 // The launch's seeds on the device (launches of more than one sample; see rmr_ctx::h_times).
-int stage_times(rmr_ctx* c, const float* times, uint32_t n, const float** out) {
+int stage_times(rmr_ctx* c, const float* times, uint32_t n, const float** out, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (n > c->times_cap) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->d_times) (void)hipFree(c->d_times);
@@ -741,7 +840,9 @@ int stage_times(rmr_ctx* c, const float* times, uint32_t n, const float** out) {
     float* h = c->h_times + c->times_pos;
     float* d = c->d_times + c->times_pos;
     std::memcpy(h, times, n * sizeof(float));
-    HIPCHK(c, hipMemcpyAsync(d, h, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    // (on a slot's stream, the copy is covered by the context stream's syncs above: the slot's trace
+    // follows it there, and the trace's fold on the context stream waits for the trace)
+    HIPCHK(c, hipMemcpyAsync(d, h, n * sizeof(float), hipMemcpyHostToDevice, st));
     c->times_pos += n;
     *out = d;
     return RMR_OK;
@@ -819,9 +920,13 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     chunk = std::min<size_t>(chunk, nspp);
     // the trace kernel indexes units with 32 bits (atomic work counter included): < 2^31 per launch
     chunk = std::max<size_t>(1, std::min<size_t>(chunk, ((size_t)1 << 31) / plane));
-    if ((r = ensure_samp(c, plane * chunk))) return r;
+    // slots for launches whose planes fit the budget shared between the slots (larger ones, C4's 34-GB
+    // 4K 256-spp frame, run on the context's stream: one plane buffer of them is enough)
+    const bool slotted = c->launch_streams >= 2 && plane * chunk * sizeof(float4) <= c->samp_budget / (size_t)c->launch_streams;
+    if (slotted && c->slots.size() != (size_t)c->launch_streams) {
+        if ((r = free_slots(c)) || (r = make_slots(c))) return r;
+    }
     const float* d_times = nullptr;
-    if (nspp > 1 && (r = stage_times(c, times, nspp, &d_times))) return r;
 
     const CompiledScene& s = c->scene;
     KParams P{};
@@ -923,9 +1028,24 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
     const int full_grid = c->n_cu * bpc;
     for (uint32_t k0 = 0; k0 < nspp; k0 += (uint32_t)chunk) {
         const uint32_t n = (uint32_t)std::min<size_t>(chunk, nspp - k0);
+        // a slot only while the previous trace is still running (something to overlap); otherwise the
+        // context's stream, with no stream hop (one launch per frame, then a sync: r06t_slot_ab.log)
+        rmr_ctx::Slot* S = nullptr;
+        if (slotted && c->trace_end && hipEventQuery(c->trace_end) == hipErrorNotReady) {
+            if ((r = slot_prepare(c, plane * n, &S))) return r;
+            P.samp = S->samp;
+            P.queue = S->queue;
+        } else {
+            if ((r = ensure_samp(c, plane * n))) return r;
+            P.samp = c->d_samp;
+            P.queue = c->d_queue;
+        }
+        d_times = nullptr;
+        if (n > 1 && (r = stage_times(c, times + k0, n, &d_times, S ? S->s : c->stream))) return r;
+        c->last_samp = P.samp;
         P.nspp = n;
         P.first_sample = first_sample + k0;
-        P.times = d_times ? d_times + k0 : nullptr;
+        P.times = d_times;
         P.time1 = times[k0];   // the seed when this launch has one sample (unit_pixel)
         P.n_units = (uint64_t)n * plane;
         // a persistent grid no larger than the launch's work: one work chunk per wave at most (a
@@ -942,7 +1062,10 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
         P.chunk_units = 0;
         if (c->kernel_mode == 0 && c->grid_per_cu <= 0) {
             const uint64_t wpb = (uint64_t)((use_jit ? c->jit.block : 256) / 64), kchunk = use_jit ? c->jit.chunk : 128;
-            const uint64_t avail = (uint64_t)std::max(1, full_grid - c->grid_reserve);
+            // slotted launches leave workgroups free for the previous launch's fold, which waits behind
+            // the next trace's persistent workgroups otherwise (and the slot's reuse behind that fold)
+            const int reserve = (S && c->grid_reserve == 0) ? c->slot_reserve : c->grid_reserve;
+            const uint64_t avail = (uint64_t)std::max(1, full_grid - reserve);
             uint64_t ck = kchunk;
             if (c->small_chunk > 0 && P.max_bounces >= 2 && P.n_units < avail * wpb * kchunk)
                 ck = std::min(kchunk, std::max<uint64_t>((uint64_t)c->small_chunk, (P.n_units + avail * wpb - 1) / (avail * wpb)));
@@ -956,24 +1079,41 @@ int render_tiles(rmr_ctx* c, const std::vector<TileXY>& tiles, int x0, int y0, i
             P.shade_threshold = use_jit ? c->jit.shade_t : 16;
             P.refill_threshold = refill_for(c->refill_threshold, P.shade_threshold);
         }
-        if (c->queue_dirty) HIPCHK(c, hipMemsetAsync(c->d_queue, 0, rmr::kQueueBytes, c->stream));
-        c->queue_dirty = true;   // until the fold that zeroes it is queued
+        const hipStream_t ts = S ? S->s : c->stream;   // the trace's stream
+        bool& qdirty = S ? S->queue_dirty : c->queue_dirty;
+        if (qdirty) HIPCHK(c, hipMemsetAsync(P.queue, 0, rmr::kQueueBytes, ts));
+        qdirty = true;   // until the fold that zeroes it is queued
         EventPair ev = get_events(c);
-        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        HIPCHK(c, hipEventRecord(ev.a, ts));
+        hipError_t le;
         if (use_jit) {
             void* args[] = {&P};
-            HIPCHK(c, hipModuleLaunchKernel(c->jit.fn, (unsigned)grid, 1, 1, (unsigned)c->jit.block, 1, 1, 0, c->stream, args,
-                                            nullptr));
-            c->stats.jit_launches++;
+            le = hipModuleLaunchKernel(c->jit.fn, (unsigned)grid, 1, 1, (unsigned)c->jit.block, 1, 1, 0, ts, args, nullptr);
+            if (le == hipSuccess) c->stats.jit_launches++;
         } else {
-            HIPCHK(c, rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, c->stream));
+            le = rmr::launch_trace(P, s.variant, c->map_np, c->has_prog, c->kernel_mode == 0, grid, ts);
         }
-        HIPCHK(c, hipEventRecord(ev.b, c->stream));
+        if (le == hipSuccess) le = hipEventRecord(ev.b, ts);
+        if (le == hipSuccess && c->launch_streams >= 2) {
+            if (!c->trace_end) le = hipEventCreateWithFlags(&c->trace_end, hipEventDisableTiming);
+            if (le == hipSuccess) le = hipEventRecord(c->trace_end, ts);
+        }
+        if (S) {
+            // the context's stream waits for the trace before its fold (and before anything after it)
+            if (le == hipSuccess) le = hipEventRecord(S->done, ts);
+            if (le == hipSuccess) le = hipStreamWaitEvent(c->stream, S->done, 0);
+            if (le != hipSuccess) (void)hipStreamSynchronize(ts);   // nothing of this slot left running
+        }
+        if (le != hipSuccess) return fail(c, RMR_E_HIP, std::string("trace launch: ") + hipGetErrorString(le));
         // (RMR_DIAG_NO_FOLD: what the fold costs the frame, a timing experiment with a wrong accumulator;
         // the next launch then zeroes the queue with a memset)
         if (!c->diag_no_fold) {
             HIPCHK(c, rmr::launch_fold(P, c->stream));
-            c->queue_dirty = false;
+            qdirty = false;
+        }
+        if (S) {
+            HIPCHK(c, hipEventRecord(S->freed, c->stream));
+            S->in_use = true;
         }
         HIPCHK(c, hipEventRecord(ev.c, c->stream));
         c->pending.push_back(ev);
@@ -1111,7 +1251,7 @@ int rmr_create(rmr_ctx** out, int device) {
     if (const char* e = RMR_ENV("RMR_GRID_PER_CU")) c->grid_per_cu = std::max(0, std::atoi(e));
     if (const char* e = RMR_ENV("RMR_GRID_RESERVE")) c->grid_reserve = std::max(0, std::atoi(e));
     if (const char* e = RMR_ENV("RMR_JIT")) c->jit_mode = std::max(0, std::min(2, std::atoi(e)));
-    if (alloc_accum(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
+    if (alloc_accum(c) != RMR_OK || make_slots(c) != RMR_OK) { rmr_destroy(c); return RMR_E_HIP; }
     *out = c;
     return RMR_OK;
 }
@@ -1120,6 +1260,7 @@ void rmr_destroy(rmr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)free_slots(c);
     for (auto& e : c->pending) c->pool.push_back(e);
     for (auto& e : c->pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); (void)hipEventDestroy(e.c); }
     void* bufs[] = {c->d_prims, c->d_ops, c->d_consts, c->d_mats, c->d_spec, c->d_rm2, c->d_dprims, c->d_dmats, c->d_bvh, c->d_esc, c->d_env, c->d_samp,
@@ -1295,6 +1436,15 @@ int rmr_set_call_batching(rmr_ctx* c, int mode) {
     RMR_FLUSH(c);
     c->call_batching = mode;
     return RMR_OK;
+}
+
+int rmr_set_launch_streams(rmr_ctx* c, int n) {
+    if (!c || n < 0 || n > 4) return RMR_E_INVALID;
+    RMR_FLUSH(c);
+    if (n == c->launch_streams) return RMR_OK;
+    int r = free_slots(c);   // (syncs the context's stream: every queued trace is done)
+    c->launch_streams = n;
+    return r ? r : make_slots(c);
 }
 
 int rmr_render_spp(rmr_ctx* c, const float* times, int x0, int y0, int x1, int y1, uint32_t first_sample, uint32_t nspp) {
@@ -1708,7 +1858,7 @@ int rmr_trace_samples(rmr_ctx* c, const float* times, int x0, int y0, int x1, in
     c->samp_budget = saved_budget;
     if (r) return r;
     std::vector<float4> h(plane * nspp);
-    HIPCHK(c, hipMemcpyAsync(h.data(), c->d_samp, h.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->last_samp, h.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int w = x1 - x0, hh = y1 - y0;
     const int tx = (w + 7) / 8;

@@ -124,7 +124,10 @@ int rmr_group_create(rmr_group** out, const int* devices, int n) {
             if (rmr_create(&mb.ctx[k], mb.device) != RMR_OK || hipSetDevice(mb.device) != hipSuccess ||
                 hipStreamCreateWithFlags(&mb.stream[k], hipStreamNonBlocking) != hipSuccess ||
                 rmr_set_stream(mb.ctx[k], (void*)mb.stream[k]) != RMR_OK ||
-                rmr_set_grid_reserve(mb.ctx[k], kGridReserve) != RMR_OK) {
+                rmr_set_grid_reserve(mb.ctx[k], kGridReserve) != RMR_OK ||
+                // the two contexts overlap each other's frames: no launch slots of their own
+                // (rmr.h rmr_set_launch_streams: 2 x 3 streams would exceed the hardware queues)
+                rmr_set_launch_streams(mb.ctx[k], 0) != RMR_OK) {
                 rmr_group_destroy(g);
                 return RMR_E_HIP;
             }

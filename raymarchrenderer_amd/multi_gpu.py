@@ -89,9 +89,10 @@ class FrameRenderer:
     one-GPU box."""
 
     def __init__(self, renderer, accums, W, H, tile, rank, world, dist=None, render_fn=None, streams=None,
-                 reduce_at_world1=False, grid_reserve=OVERLAP_GRID_RESERVE):
+                 reduce_at_world1=False, grid_reserve=OVERLAP_GRID_RESERVE, launch_streams=None):
         self.rs = list(renderer) if isinstance(renderer, (list, tuple)) else [renderer]
         self._saved_reserve = []
+        self._saved_streams = []
         if render_fn is None and len(self.rs) > 1 and grid_reserve is not None:
             # overlapping contexts: each trace launch leaves a few workgroup slots free, so the other
             # context's fold and zeroing run beside it instead of waiting for its drain (rmr.h); the
@@ -99,6 +100,15 @@ class FrameRenderer:
             for r in self.rs:
                 self._saved_reserve.append((r, r.grid_reserve))
                 r.set_grid_reserve(grid_reserve)
+        if render_fn is None and (launch_streams is not None or len(self.rs) > 1):
+            # overlapping contexts already fill each other's drains: no launch slots of their own by
+            # default (rmr.h rmr_set_launch_streams; 2 contexts x 3 streams exceed the 4 hardware
+            # queues: r06p_launch_streams.log, RM3 -10%, C1 -28%); restored at close()
+            n = launch_streams if launch_streams is not None else 0
+            for r in self.rs:
+                if r.launch_streams != n:
+                    self._saved_streams.append((r, r.launch_streams))
+                    r.set_launch_streams(n)
         self.r, self.dist, self.render_fn = self.rs[0], dist, render_fn
         self.accs = list(accums) if isinstance(accums, (list, tuple)) else [accums]
         if len(self.accs) % len(self.rs):
@@ -233,10 +243,14 @@ class FrameRenderer:
         return self.last
 
     def close(self):
-        """finish(), then give the renderers back their grid reserve from before this FrameRenderer
-        (the passed contexts can be used on their own or in another FrameRenderer afterwards)."""
+        """finish(), then give the renderers back their grid reserve and launch streams from before this
+        FrameRenderer (the passed contexts can be used on their own or in another FrameRenderer
+        afterwards)."""
         last = self.finish()
         for r, v in self._saved_reserve:
             r.set_grid_reserve(v)
         self._saved_reserve = []
+        for r, v in self._saved_streams:
+            r.set_launch_streams(v)
+        self._saved_streams = []
         return last

@@ -211,6 +211,17 @@ class Renderer:
         and accumulator). Batched render() calls go to the GPU together at the next other call."""
         self._chk(self._L.rmr_set_call_batching(self._ctx, int(mode)))
 
+    def set_launch_streams(self, n):
+        """rmr_set_launch_streams: n >= 2 (the library's default 2) overlaps consecutive trace launches on
+        n private streams (one sample-plane buffer each); 0 runs them on the context's stream. Same bits."""
+        self._chk(self._L.rmr_set_launch_streams(self._ctx, int(n)))
+        self._launch_streams = int(n)
+
+    @property
+    def launch_streams(self):
+        """The last set_launch_streams value (rmr_api.cpp's default 2 before any)."""
+        return getattr(self, "_launch_streams", 2)
+
     def render_spp(self, times, rect=None, first_sample=0):
         times = np.ascontiguousarray(times, np.float32)
         if rect is None:

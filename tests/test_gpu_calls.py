@@ -178,3 +178,89 @@ def test_small_launch_claims_keep_results(monkeypatch):
     acc = o.render([times[0]], rect=(0, 0, 48, 40))   # a corner of the first call's tile
     acc = o.render([times[1]], rect=(7, 3, 37, 23), first_sample=1, accum=acc)
     assert same_bits(out["64"][:40, :48], acc[:40, :48]).all()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launch_streams_bitwise(renderer, n):
+    """rmr_set_launch_streams: consecutive trace launches on n private streams (own planes and work
+    queue each), folds in call order on the context's stream. One launch per call (the reference's
+    fixed loop, call batching off), chunked launches (a small sample-plane budget: 3 + 3 + 1 samples
+    per render), frames separated by reloads and per-sample planes (rmr_trace_samples) all give the bits
+    of the one-stream context, and the oracle's."""
+    W, H, gw, gh = 62, 45, 3, 4
+    prm, view = _setup(renderer, CORNELL, "rm1", W, H, {"max_bounces": 3})
+    times = time_schedule(4, frame=3)
+    rects = _rects(W, H, gw, gh)
+    runs = {}
+    try:
+        renderer.set_call_batching(0)
+        for ls in (0, n):
+            renderer.set_launch_streams(ls)
+            renderer.reload()
+            renderer.reset_stats()
+            _fixed(renderer, rects, times)
+            calls = renderer.read_accum()
+            assert renderer.stats().trace_launches == len(rects) * len(times)
+            frames = []
+            for f in range(3):   # frame after frame on one context (rmr_render_spp), reload between
+                renderer.reload()
+                renderer.render_spp(time_schedule(7, frame=f))
+                frames.append(renderer.read_accum())
+            plane_bytes = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 16
+            renderer.set_tuning(samp_budget=3 * plane_bytes)
+            renderer.reload()
+            renderer.reset_stats()
+            renderer.render_spp(time_schedule(7, frame=5))
+            chunked = renderer.read_accum()
+            assert renderer.stats().trace_launches == 3
+            renderer.set_tuning(samp_budget=48 << 30)   # the default (rmr_api.cpp)
+            planes = renderer.trace_samples(time_schedule(3, frame=6), (5, 4, 29, 21))
+            runs[ls] = (calls, frames, chunked, planes)
+    finally:
+        renderer.set_launch_streams(0)
+        renderer.set_call_batching(-1)
+        renderer.set_tuning(samp_budget=48 << 30)
+    a, b = runs[0], runs[n]
+    assert same_bits(a[0], b[0]).all()
+    for x, y in zip(a[1], b[1]):
+        assert same_bits(x, y).all()
+    assert same_bits(a[2], b[2]).all() and same_bits(a[3], b[3]).all()
+    cw, ch = W // gw, H // gh
+    o = oracle.Oracle(_tables(CORNELL, "rm1"), prm, view, W, H)
+    assert same_bits(b[0], o.render(times, rect=(0, 0, cw * gw, ch * gh))).all()
+    assert same_bits(b[1][2], o.render(time_schedule(7, frame=2))).all()
+
+
+def test_launch_streams_on_a_caller_stream():
+    """With a caller's stream and accumulator (FrameRenderer's way) the traces run on the context's
+    private streams, but each call's fold is on the caller's stream: work ordered after the call there
+    sees the sample, with no other synchronisation."""
+    import torch
+    r = Renderer(0, 32, 24)
+    try:
+        r.load_scene(CORNELL, "rm1")
+        r.set_params(abi.default_params(max_bounces=2))
+        r.set_launch_streams(2)
+        s = torch.cuda.Stream()
+        acc = torch.zeros((24, 32, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.set_stream(s.cuda_stream)
+        r.bind_accum(acc.data_ptr(), acc.numel() * 4)
+        times = time_schedule(6, frame=1)
+        for k, t in enumerate(times):
+            r.render(float(t), (0, 0), (32, 24), k)
+        with torch.cuda.stream(s):
+            snap = acc.clone()   # ordered after the last call's fold on the caller's stream
+        s.synchronize()
+        got = snap.cpu().numpy()
+        r2 = Renderer(0, 32, 24)
+        try:
+            r2.load_scene(CORNELL, "rm1")
+            r2.set_params(abi.default_params(max_bounces=2))
+            r2.render_spp(times)
+            want = r2.read_accum()
+        finally:
+            r2.close()
+        assert same_bits(got, want).all()
+    finally:
+        r.close()
