@@ -1282,6 +1282,8 @@ int rmr_set_stream(rmr_ctx* c, void* s) {
     if (!c) return RMR_E_INVALID;
     RMR_FLUSH(c);
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    int r = free_slots(c);   // (every queued trace done)
+    if (r) return r;
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     if (s) {
         c->stream = (hipStream_t)s;
@@ -1290,7 +1292,9 @@ int rmr_set_stream(rmr_ctx* c, void* s) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
     }
-    return RMR_OK;
+    // the slots' streams again, created after the context's stream (HIP hands out its hardware queues
+    // in creation order: r06v_set_stream_slots.log)
+    return make_slots(c);
 }
 
 int rmr_set_image_size(rmr_ctx* c, int w, int h) {
