@@ -2292,7 +2292,9 @@ constexpr int trace_waves() {
 #define RMR_CHUNK 128   // units a wave takes from the work queue at a time (primary rays in LDS)
 #endif
 #ifndef RMR_QUEUE_PARTS
-#define RMR_QUEUE_PARTS 16   // work-queue partitions (counters; rmr_internal.h kQueueBytes)
+#define RMR_QUEUE_PARTS 32   // work-queue partitions (counters; rmr_internal.h kQueueBytes): 32 against
+                             // 16, same process: RM3 -0.5 / -3.5% at 16 / 4 spp, RM2 -2%, C3 -1.2%, the
+                             // rest within noise (r06z2_parts_ab.log, r06z4_parts_ab2.log)
 #endif
 #ifndef RMR_QUEUE_SEQ
 #define RMR_QUEUE_SEQ 1   // small launches: partitions a wave tries in turn before it reads every counter
@@ -2333,7 +2335,7 @@ RMR_D void trace_main(const KParams& P) {
     const uint32_t CK = P.chunk_units - 1u < CHUNK ? P.chunk_units : CHUNK;
     uint32_t rnext = 0, rend = 0;
     // The work queue in RMR_QUEUE_PARTS partitions of whole chunks, each with its own counter (128 B
-    // apart): a wave starts on partition blockIdx % parts (with 8 or 16 partitions, blocks of one XCD
+    // apart): a wave starts on partition blockIdx % parts (with a multiple of 8 partitions, blocks of one XCD
     // under the round-robin block dispatch over the 8 XCDs) and moves on to the next partition when
     // its own is used up. One counter shared by every wave of the chip serialises its atomics: RM2's
     // short paths fetch ~80 chunks per microsecond, and one counter held its 1080p 16-spp frame at
@@ -2374,6 +2376,7 @@ RMR_D void trace_main(const KParams& P) {
 #ifdef RMR_PROFILE
     uint64_t cyc[4] = {0, 0, 0, 0};   // refill, map() iterations, shading, cache kernels: full map() batches
     uint64_t full_lanes = 0;           // cache kernels: lanes in the full map() batches
+    uint64_t cyc_claim = 0, cyc_rays = 0;   // refill: work-queue claims (atomics), chunk primary rays
     const uint64_t c_begin = __builtin_amdgcn_s_memtime();
 #define RMR_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #else
@@ -2433,6 +2436,9 @@ RMR_D void trace_main(const KParams& P) {
                     // cyclic order) whose counter says it has work left — all counters read at once, one
                     // per lane — until none has (the launch's work is all handed out)
                     unsigned int base = 0;
+#ifdef RMR_PROFILE
+                    const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
                     for (;;) {
                         const uint32_t pb = part_begin(part), pe = part_begin(part + 1);
                         unsigned int off = 0;
@@ -2472,6 +2478,10 @@ RMR_D void trace_main(const KParams& P) {
                         part = (uint32_t)__builtin_ctzll(m);
                     }
                     rnext = base;
+#ifdef RMR_PROFILE
+                    const uint64_t q1 = __builtin_amdgcn_s_memtime();
+                    cyc_claim += q1 - q0;
+#endif
 #ifdef RMR_WAVE_TIMES   // diagnostics (tools/wave_times.py): when each wave finds the queue empty
                     if (exhausted && lane_now() == 0) {
                         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
@@ -2486,6 +2496,9 @@ RMR_D void trace_main(const KParams& P) {
                             if (base + sl < rend) s_ray[wv][sl] = chunk_ray<HO>(P, base + sl);
                         }
                         __builtin_amdgcn_wave_barrier();
+#ifdef RMR_PROFILE
+                        cyc_rays += __builtin_amdgcn_s_memtime() - q1;
+#endif
                     }
                 }
                 if (!exhausted) {
@@ -2802,6 +2815,8 @@ RMR_D void trace_main(const KParams& P) {
             atomicAdd(P.counters + 9, (unsigned long long)cyc[3]);
             atomicAdd(P.counters + 10, (unsigned long long)full_lanes);
         }
+        atomicAdd(P.counters + 11, (unsigned long long)cyc_claim);
+        atomicAdd(P.counters + 12, (unsigned long long)cyc_rays);
         atomicAdd(P.counters + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c_begin));
 #endif
     }

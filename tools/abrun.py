@@ -144,7 +144,9 @@ def main():
                 # as fractions of the waves' cycles (the s_memtime stamps themselves cost ~10%)
                 c, tot = cnt[i], max(1, cnt[i][7])
                 out[v["label"]]["sections"] = {"refill": round(c[4] / tot, 4), "map_loop": round(c[5] / tot, 4),
-                                               "shade": round(c[6] / tot, 4), "cache_full_maps": round(c[9] / tot, 4)}
+                                               "shade": round(c[6] / tot, 4), "cache_full_maps": round(c[9] / tot, 4),
+                                               # parts of refill: work-queue claims, the chunk's primary rays
+                                               "refill_claims": round(c[11] / tot, 4), "refill_rays": round(c[12] / tot, 4)}
                 if c[3]:   # cache kernels: lanes per full map() batch (counter 10 of the profiling build)
                     out[v["label"]]["lanes_per_full_batch"] = round(c[10] / c[3], 2)
         print(json.dumps(out), flush=True)
