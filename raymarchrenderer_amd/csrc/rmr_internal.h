@@ -47,9 +47,10 @@ struct BvhNode {
 };
 
 // the trace kernel's work-queue counters (rmr_trace.h RMR_QUEUE_PARTS partitions, 128 B apart; room
-// for 64): zero when a trace launch starts. Zeroed once at rmr_create, then by each launch's fold
-// (fold_main, after its trace on the same stream) for the next launch, so a launch costs no separate
-// memset dispatch (the reference's one-sample Graphics::Render calls: one dispatch fewer per call)
+// for 64): zero when a trace launch starts. Zeroed once at rmr_create (and at a launch slot's creation),
+// then by each launch's fold (fold_main, ordered after its trace) for the next launch on the same queue,
+// so a launch costs no separate memset dispatch (the reference's one-sample Graphics::Render calls: one
+// dispatch fewer per call)
 constexpr size_t kQueueBytes = 8192;
 constexpr int kQueueWordStride = 32;   // 32-bit words between two partition counters
 
