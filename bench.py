@@ -109,7 +109,7 @@ def parse():
     ap.add_argument("--overlap", type=int, default=-1,
                     help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU; "
                          "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
-                         "+97%% C1, round 3). The roofline's per-launch time then comes from "
+                         "+97%% C1, round 3; default_overlap). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
     ap.add_argument("--grid-reserve", type=int, default=-1,
                     help="with overlapping contexts, workgroups each trace launch leaves free for the other "
@@ -383,6 +383,16 @@ def combined_stats(rs):
     return out
 
 
+def default_overlap(cfg, spp, world):
+    """--overlap's default: contexts - 1 on the frame path, two contexts. Three measured faster on
+    short frames in a lean process (C1 +42%, RM2 +9%, RM3 +2%, the 8-rank C2 share's prediction 7.33x
+    -> 7.41x; r06z8_overlap3.log), but slower in the full bench line (C1 856 against 1,117, RM3 2,842
+    against 3,082; r06z9_bench_*): three contexts' streams and torch's default stream fill the 4
+    hardware queues a process gets, and any further stream (the count pass's, the PSNR check's)
+    makes two of them share a queue."""
+    return 1
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -541,7 +551,7 @@ def predict_partition(args, cfg):
     W, H = cfg["W"], cfg["H"]
     spp = args.spp or cfg["spp"]
     animated = bool(cfg.get("animated"))
-    n_ctx = (args.overlap if args.overlap >= 0 else 1) + 1   # renderer contexts (as main(): --overlap)
+    n_ctx = (args.overlap if args.overlap >= 0 else 1) + 1   # renderer contexts (--overlap; default two)
     rs, streams = [], []
     for _ in range(n_ctx):
         r = Renderer(0, W, H)
@@ -811,11 +821,15 @@ def main():
     # chip) overlaps the next frame's start (multi_gpu.FrameRenderer). Default on: a
     # renderer producing frame after frame pipelines them; it pays most where frames are short
     # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1).
-    overlap = args.overlap if args.overlap >= 0 else 1
+    overlap = args.overlap if args.overlap >= 0 else default_overlap(cfg, spp, world)
     n_ctx = overlap + 1 if overlap > 0 else 1
     rs, streams = [], []
     for _ in range(n_ctx):
         r = Renderer(local_rank, W, H)
+        if n_ctx > 1 and args.launch_streams < 0:
+            # overlapping contexts take no launch slots (FrameRenderer sets the same): dropped before
+            # the context's torch stream exists, so the hardware queues go to the contexts' streams
+            r.set_launch_streams(0)
         load_into(r, cfg, scene_for_frame(cfg, 0))
         r.set_params(abi.default_params(max_bounces=BOUNCES))
         if args.kernel:
