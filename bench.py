@@ -41,6 +41,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's GPU_MAX_HW_QUEUES, default 4; the GPU box exports 4), raised to 8
+# before anything initialises HIP: the frame path's overlapping contexts each need their stream on a
+# queue of its own, and with 4 the third context's stream (or RCCL's) shares one and serialises behind
+# another context's trace (C1 856 against 1,637 Msamples/s with three contexts; r06za_hwq.log). A
+# caller's value of 8 or more is kept.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = "Msamples/sec (pixels×spp) at 1920×1080; PSNR vs GLSL reference"
 TILE = 32
@@ -108,8 +115,9 @@ def parse():
     ap.add_argument("--traffic-json", default="")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU; "
-                         "0: one context; default 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, "
-                         "+97%% C1, round 3; default_overlap). The roofline's per-launch time then comes from "
+                         "0: one context; default 2 (three contexts) where a rank's frame share is <= 20 M samples, "
+                         "else 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, +97%% C1, round 3; "
+                         "default_overlap). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
     ap.add_argument("--grid-reserve", type=int, default=-1,
                     help="with overlapping contexts, workgroups each trace launch leaves free for the other "
@@ -384,13 +392,14 @@ def combined_stats(rs):
 
 
 def default_overlap(cfg, spp, world):
-    """--overlap's default: contexts - 1 on the frame path, two contexts. Three measured faster on
-    short frames in a lean process (C1 +42%, RM2 +9%, RM3 +2%, the 8-rank C2 share's prediction 7.33x
-    -> 7.41x; r06z8_overlap3.log), but slower in the full bench line (C1 856 against 1,117, RM3 2,842
-    against 3,082; r06z9_bench_*): three contexts' streams and torch's default stream fill the 4
-    hardware queues a process gets, and any further stream (the count pass's, the PSNR check's)
-    makes two of them share a queue."""
-    return 1
+    """--overlap's default: contexts - 1 on the frame path. Three contexts where a rank's share of a
+    frame is short (<= 20 M samples: C1 1,123 -> 1,637 Msamples/s, RM2 25,659 -> 27,959, RM3 3,094 ->
+    3,153 with 8 hardware queues, r06za_hwq.log; the 8-rank C2 share's prediction 7.33x -> 7.41x,
+    r06z8_overlap3.log), two elsewhere (C2 at N = 1: 2,896 with two, 2,877 with three). Three
+    contexts need GPU_MAX_HW_QUEUES above 4 (set at the top of this file): with 4 they were slower
+    than two (C1 856)."""
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    return 2 if queues >= 8 and cfg["W"] * cfg["H"] * spp / max(1, world) <= 20e6 else 1
 
 
 def free_port():
@@ -820,7 +829,7 @@ def main():
     # one frame's trace-kernel drain (~1.2 ms of a persistent kernel's last paths on a nearly idle
     # chip) overlaps the next frame's start (multi_gpu.FrameRenderer). Default on: a
     # renderer producing frame after frame pipelines them; it pays most where frames are short
-    # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1).
+    # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1), where three contexts pay more again.
     overlap = args.overlap if args.overlap >= 0 else default_overlap(cfg, spp, world)
     n_ctx = overlap + 1 if overlap > 0 else 1
     rs, streams = [], []
