@@ -115,7 +115,7 @@ def parse():
     ap.add_argument("--traffic-json", default="")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="K >= 1: K + 1 renderer contexts on as many streams, consecutive frames overlap on the GPU; "
-                         "0: one context; default 2 (three contexts) where a rank's frame share is <= 20 M samples, "
+                         "0: one context; default 3 (four contexts) where a rank's frame share is <= 20 M samples, "
                          "else 1 (two contexts: at N = 1 +1.3%% C2, +25%% RM3, +18%% RM2, +97%% C1, round 3; "
                          "default_overlap). The roofline's per-launch time then comes from "
                          "`steps` frames rendered one at a time after the timed region")
@@ -392,14 +392,16 @@ def combined_stats(rs):
 
 
 def default_overlap(cfg, spp, world):
-    """--overlap's default: contexts - 1 on the frame path. Three contexts where a rank's share of a
-    frame is short (<= 20 M samples: C1 1,123 -> 1,637 Msamples/s, RM2 25,659 -> 27,959, RM3 3,094 ->
-    3,153 with 8 hardware queues, r06za_hwq.log; the 8-rank C2 share's prediction 7.33x -> 7.41x,
-    r06z8_overlap3.log), two elsewhere (C2 at N = 1: 2,896 with two, 2,877 with three). Three
-    contexts need GPU_MAX_HW_QUEUES above 4 (set at the top of this file): with 4 they were slower
-    than two (C1 856)."""
+    """--overlap's default: contexts - 1 on the frame path. Four contexts where a rank's share of a
+    frame is short (<= 20 M samples), two elsewhere, with 8 hardware queues:
+      C1: 1,123 (two) / 1,620 (three) / 2,047 (four) / 1,403 (five) Msamples/s;
+      RM2: 25,659 / 27,814 / 29,422 / 29,279; RM3: 3,094 / 3,131 / 3,132 / 3,055
+      (r06za_hwq.log, r06zc_ctx45.log); the 8-rank C2 share: 6.22 / 6.15 / 6.10 ms (r06zd_predict_ctx.log);
+      C2 at N = 1: 2,902 (two) against 2,889 (three) (r06zb_hwq_long.log).
+    More than two contexts need GPU_MAX_HW_QUEUES above 4 (set at the top of this file): with 4, three
+    were slower than two (C1 856)."""
     queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-    return 2 if queues >= 8 and cfg["W"] * cfg["H"] * spp / max(1, world) <= 20e6 else 1
+    return 3 if queues >= 8 and cfg["W"] * cfg["H"] * spp / max(1, world) <= 20e6 else 1
 
 
 def free_port():
@@ -829,7 +831,7 @@ def main():
     # one frame's trace-kernel drain (~1.2 ms of a persistent kernel's last paths on a nearly idle
     # chip) overlaps the next frame's start (multi_gpu.FrameRenderer). Default on: a
     # renderer producing frame after frame pipelines them; it pays most where frames are short
-    # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1), where three contexts pay more again.
+    # (RM3 / RM2 4 spp, C1, a rank's 1/N of a frame at N > 1), where four contexts pay more again.
     overlap = args.overlap if args.overlap >= 0 else default_overlap(cfg, spp, world)
     n_ctx = overlap + 1 if overlap > 0 else 1
     rs, streams = [], []

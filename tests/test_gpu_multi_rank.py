@@ -40,7 +40,7 @@ def test_share_gpu_ranks_reduce_bitexact(gpus, config, spp):
     assert all(p["trace_launches"] > 0 for p in mg["per_rank"])
     assert sum(p["tiles32"] for p in mg["per_rank"]) == 60 * 34
     assert mg["verify"]["bitwise_equal_to_one_context"] is True, mg["verify"]
-    assert out["config"]["frame_streams"] == 3   # a rank's share <= 20 M samples (bench.default_overlap)
+    assert out["config"]["frame_streams"] == 4   # a rank's share <= 20 M samples (bench.default_overlap)
 
 
 @pytest.mark.gpu
@@ -68,7 +68,7 @@ def test_default_line_overlaps_frames_and_times_launches_solo():
     """bench.py's default N = 1 line: two renderer contexts whose consecutive frames overlap (the
     value), and the roofline's per-launch time from frames rendered one at a time afterwards."""
     out = _run("--config", "c1", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-psnr")
-    assert out["n_gpus"] == 1 and out["config"]["frame_streams"] == 3   # C1: three contexts (default_overlap)
+    assert out["n_gpus"] == 1 and out["config"]["frame_streams"] == 4   # C1: four contexts (default_overlap)
     roof = out["roofline"]
     assert "one at a time" in roof["note"]
     assert 0 < roof["avg_launch_ms"] < 5 and roof["map_evals_per_launch"] > 0
