@@ -701,6 +701,7 @@ def api_render_bench(args, cfg):
         r.render_spp(times, rect=(0, 0, cw * gw, ch * gh))
     r.sync()
     batched = samples / (time.perf_counter() - tb) / 1e6
+    slots = r.launch_streams
     r.close()
     ms_step = elapsed / args.steps * 1e3
     out = {"metric": METRIC, "value": round(samples / elapsed / 1e6, 2), "unit": "Msamples/s", "n_gpus": 1,
@@ -710,7 +711,7 @@ def api_render_bench(args, cfg):
                                   "(Program.cpp fixed-spp loop)" % (cfg["name"], W, H, spp, cfg["bounces"]),
                       "config": args.config, "api": "render", "grid": "%dx%d" % (gw, gh), "tile_px": [cw, ch],
                       "order": "spiral (Program.cpp:203-222)", "call_batching": args.call_batching,
-                      "launch_streams": r.launch_streams,
+                      "launch_streams": slots,
                       "width": W, "height": H, "spp": spp,
                       "max_bounces": cfg["bounces"]},
            "calls": {"per_step": len(rects) * spp, "per_s": round(calls / elapsed, 1),

@@ -136,7 +136,7 @@ int rmr_render(rmr_ctx* ctx, float time, float min_x, float min_y, float max_x, 
  * the context owns its stream and its accumulator (no rmr_set_stream / rmr_bind_accum), since only
  * then are all readers inside rmr. rmr_destroy drops calls still held. */
 int rmr_set_call_batching(rmr_ctx* ctx, int mode);
-/* Launch overlap: n >= 2 (default 2) puts consecutive trace launches round-robin on n private
+/* Launch overlap: n >= 2 (default 2; 4 with 8 or more hardware queues) puts consecutive trace launches round-robin on n private
  * streams, each with its own sample planes and work queue, so one launch's drain (its last long paths)
  * overlaps the next launch's start; n = 0 or 1 runs every launch on the context's stream. Each
  * launch's fold stays on the context's stream, after its trace and in call order, so results are
@@ -146,6 +146,9 @@ int rmr_set_call_batching(rmr_ctx* ctx, int mode);
  * (multi_gpu.FrameRenderer, the device group) set 0: their streams would exceed the GPU's hardware
  * queues (4 per process) and serialise. */
 int rmr_set_launch_streams(rmr_ctx* ctx, int n);
+/* The context's launch streams (rmr_create's default: 2, or 4 where the process has 8 or more hardware
+ * queues, GPU_MAX_HW_QUEUES); -1 for a null context. */
+int rmr_get_launch_streams(const rmr_ctx* ctx);
 /* Batched fast path: samples first_sample .. first_sample+nspp-1 of every pixel in the integer
  * rect [x0,x1)x[y0,y1), sample k seeded with times[k]. Bitwise equal to nspp rmr_render calls
  * with the same times. */

@@ -25,7 +25,7 @@ EXPORTS = [
     "rmr_save_accum", "rmr_load_accum", "rmr_sync", "rmr_get_stats", "rmr_reset_stats", "rmr_get_section_cycles", "rmr_get_counters", "rmr_set_culling",
     "rmr_set_kernel", "rmr_set_tuning", "rmr_set_grid_reserve", "rmr_trace_samples", "rmr_abi_sizes", "rmr_set_jit", "rmr_set_instrument", "rmr_jit_compile_scene", "rmr_set_env_map",
     "rmr_scene_compile", "rmr_scene_view", "rmr_scene_free", "rmr_display", "rmr_display_device",
-    "rmr_srgb_thresholds", "rmr_candidate_grid", "rmr_set_call_batching", "rmr_set_launch_streams",
+    "rmr_srgb_thresholds", "rmr_candidate_grid", "rmr_set_call_batching", "rmr_set_launch_streams", "rmr_get_launch_streams",
 ]
 
 
@@ -106,6 +106,7 @@ def lib(diag=None):
         "rmr_set_grid_reserve": (C.c_int, [vp, C.c_int]),
         "rmr_set_call_batching": (C.c_int, [vp, C.c_int]),
         "rmr_set_launch_streams": (C.c_int, [vp, C.c_int]),
+        "rmr_get_launch_streams": (C.c_int, [vp]),
         "rmr_set_jit": (C.c_int, [vp, C.c_int]),
         "rmr_set_instrument": (C.c_int, [vp, C.c_int]),
         "rmr_set_env_map": (C.c_int, [vp, C.c_void_p, C.c_int, C.c_int]),

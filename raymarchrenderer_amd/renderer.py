@@ -212,15 +212,16 @@ class Renderer:
         self._chk(self._L.rmr_set_call_batching(self._ctx, int(mode)))
 
     def set_launch_streams(self, n):
-        """rmr_set_launch_streams: n >= 2 (the library's default 2) overlaps consecutive trace launches on
-        n private streams (one sample-plane buffer each); 0 runs them on the context's stream. Same bits."""
+        """rmr_set_launch_streams: n >= 2 (the library's default: 2, or 4 with 8 or more hardware queues)
+        overlaps consecutive trace launches on n private streams (one sample-plane buffer each); 0 runs
+        them on the context's stream. Same bits."""
         self._chk(self._L.rmr_set_launch_streams(self._ctx, int(n)))
-        self._launch_streams = int(n)
 
     @property
     def launch_streams(self):
-        """The last set_launch_streams value (rmr_api.cpp's default 2 before any)."""
-        return getattr(self, "_launch_streams", 2)
+        """rmr_get_launch_streams: the context's launch streams (default 2, or 4 with 8 or more hardware
+        queues per process)."""
+        return int(self._L.rmr_get_launch_streams(self._ctx))
 
     def render_spp(self, times, rect=None, first_sample=0):
         times = np.ascontiguousarray(times, np.float32)

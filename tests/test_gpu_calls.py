@@ -192,6 +192,7 @@ def test_launch_streams_bitwise(renderer, n):
     times = time_schedule(4, frame=3)
     rects = _rects(W, H, gw, gh)
     runs = {}
+    ls0 = renderer.launch_streams
     try:
         renderer.set_call_batching(0)
         for ls in (0, n):
@@ -217,7 +218,7 @@ def test_launch_streams_bitwise(renderer, n):
             planes = renderer.trace_samples(time_schedule(3, frame=6), (5, 4, 29, 21))
             runs[ls] = (calls, frames, chunked, planes)
     finally:
-        renderer.set_launch_streams(0)
+        renderer.set_launch_streams(ls0)
         renderer.set_call_batching(-1)
         renderer.set_tuning(samp_budget=48 << 30)
     a, b = runs[0], runs[n]

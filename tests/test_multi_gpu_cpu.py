@@ -133,10 +133,11 @@ def test_overlapped_frames_two_streams_bitexact():
             rs.append(r)
             streams.append(s)
         accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
-        assert all(r.launch_streams == 2 for r in rs)   # the library's default launch slots
+        ls0 = rs[0].launch_streams   # the library's default launch slots (2, or 4 with 8 hardware queues)
+        assert ls0 >= 2 and all(r.launch_streams == ls0 for r in rs)
         fr = FrameRenderer(rs, accs, W, H, tile, 0, 1, streams=streams if n_ctx > 1 else None)
         # two overlapping contexts take no launch slots (rmr.h rmr_set_launch_streams); one keeps them
-        assert all(r.launch_streams == (0 if n_ctx > 1 else 2) for r in rs)
+        assert all(r.launch_streams == (0 if n_ctx > 1 else ls0) for r in rs)
         out = []
         for f in range(4):
             acc = fr.frame(time_schedule(3, frame=f))
@@ -146,7 +147,7 @@ def test_overlapped_frames_two_streams_bitexact():
                 out.append(accs[0].cpu().numpy().view(np.uint32).copy())
                 out.append(acc.cpu().numpy().view(np.uint32).copy())
         fr.close()
-        assert all(r.launch_streams == 2 for r in rs)   # given back at close()
+        assert all(r.launch_streams == ls0 for r in rs)   # given back at close()
         for r in rs:
             r.close()
         return out
