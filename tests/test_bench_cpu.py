@@ -40,3 +40,23 @@ def test_bench_rejects_mismatched_launcher():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode != 0 and "--gpus 2" in p.stderr
+
+
+def test_default_contexts_and_hardware_queues(monkeypatch):
+    """bench.default_overlap: four overlapping contexts for a rank's frame share of <= 20 M samples
+    when the process has 8 hardware queues (bench.py raises GPU_MAX_HW_QUEUES to 8 at import), two
+    otherwise; with HIP's default 4 queues always two (three were slower: DESIGN.md §5)."""
+    sys.path.insert(0, ROOT)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    import importlib
+    import bench
+    bench = importlib.reload(bench)   # (the module-level raise runs again with this environment)
+    assert int(os.environ["GPU_MAX_HW_QUEUES"]) == 8
+    c = bench.CONFIGS
+    assert bench.default_overlap(c["c1"], 1, 1) == 3
+    assert bench.default_overlap(c["rm2"], 4, 1) == 3 and bench.default_overlap(c["rm3"], 4, 1) == 3
+    assert bench.default_overlap(c["c2"], 64, 1) == 1 and bench.default_overlap(c["c2"], 64, 4) == 1
+    assert bench.default_overlap(c["c2"], 64, 8) == 3   # the 8-rank share: 16.6 M samples
+    assert bench.default_overlap(c["c4"], 256, 8) == 1
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert bench.default_overlap(c["c1"], 1, 1) == 1
